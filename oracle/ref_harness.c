@@ -1,0 +1,149 @@
+/*
+ * ref_harness.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * Thin driver linked against the reference's own src/c library (built from
+ * /root/reference/src/c by oracle/Makefile into oracle/_ref/).  Two uses:
+ *
+ *   1. ref_encode_pair(): the reference's CLI chain main.c:257-292
+ *      (delta_crc64_xz x2 -> delta_diff -> delta_place_commands ->
+ *      delta_encode) for one in-memory pair.  tests/ call it through ctypes to
+ *      pin the oracle restatement against the real reference.
+ *   2. ref_bench main(): the CPU baseline timed by bench.py's cpu_baseline
+ *      leg — a pthread pool, one pair per task, same synthetic inputs and
+ *      table size as the GPU run, CRC table warmed first (delta.h:297-312 is
+ *      not thread-safe on first use).
+ *
+ * Nothing here is part of the product.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "delta.h"   /* the reference header, via -I$(REF) (oracle/Makefile) */
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "delta_oracle.h"
+
+size_t ref_encode_pair(int algo, const uint8_t *r, size_t r_len,
+                       const uint8_t *v, size_t v_len, size_t p,
+                       size_t q, size_t buf_cap, size_t max_table,
+                       uint8_t **out)
+{
+	uint8_t sc[DELTA_CRC_SIZE], dc[DELTA_CRC_SIZE];
+	delta_diff_options_t o = DELTA_DIFF_OPTIONS_DEFAULT;
+	o.p = p;
+	o.q = q;
+	o.buf_cap = buf_cap;
+	o.max_table = max_table;
+	delta_crc64_xz(r, r_len, sc);
+	delta_crc64_xz(v, v_len, dc);
+	delta_commands_t cmds = delta_diff((delta_algorithm_t)algo, r, r_len, v, v_len, &o);
+	delta_placed_commands_t placed = delta_place_commands(&cmds);
+	delta_buffer_t b = delta_encode(&placed, false, v_len, sc, dc);
+	delta_placed_commands_free(&placed);
+	delta_commands_free(&cmds);
+	*out = b.data;
+	return b.len;
+}
+
+void ref_free(void *p) { free(p); }
+
+#ifdef REF_BENCH_MAIN
+/* ── CPU baseline ───────────────────────────────────────────────────────── */
+
+typedef struct {
+	int algo;
+	size_t n_pairs, len, p, q;
+	uint8_t **r, **v;
+	size_t next;
+	pthread_mutex_t mu;
+	unsigned long long out_bytes;
+} job_t;
+
+static void *worker(void *arg)
+{
+	job_t *j = arg;
+	unsigned long long ob = 0;
+	for (;;) {
+		pthread_mutex_lock(&j->mu);
+		size_t i = j->next++;
+		pthread_mutex_unlock(&j->mu);
+		if (i >= j->n_pairs) break;
+		uint8_t *d = NULL;
+		ob += ref_encode_pair(j->algo, j->r[i], j->len, j->v[i], j->len,
+		                      j->p, j->q, DELTA_BUF_CAP,
+		                      DELTA_MAX_TABLE_SIZE, &d);
+		free(d);
+	}
+	pthread_mutex_lock(&j->mu);
+	j->out_bytes += ob;
+	pthread_mutex_unlock(&j->mu);
+	return NULL;
+}
+
+static double now(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return t.tv_sec + t.tv_nsec / 1e9;
+}
+
+/* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps */
+int main(int argc, char **argv)
+{
+	if (argc < 9) {
+		fprintf(stderr, "usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps\n");
+		return 2;
+	}
+	job_t j;
+	memset(&j, 0, sizeof(j));
+	j.algo = atoi(argv[1]);
+	j.n_pairs = strtoull(argv[2], NULL, 0);
+	j.len = strtoull(argv[3], NULL, 0);
+	double rate = atof(argv[4]);
+	unsigned long long seed = strtoull(argv[5], NULL, 0);
+	int threads = atoi(argv[6]);
+	j.q = strtoull(argv[7], NULL, 0);
+	int reps = atoi(argv[8]);
+	j.p = DELTA_SEED_LEN;
+	j.r = malloc(j.n_pairs * sizeof(uint8_t *));
+	j.v = malloc(j.n_pairs * sizeof(uint8_t *));
+	unsigned long long n_edits = (unsigned long long)(rate * (double)j.len + 0.5);
+	for (size_t i = 0; i < j.n_pairs; i++) {
+		j.r[i] = malloc(j.len);
+		j.v[i] = malloc(j.len);
+		or_synth_random(seed + i, j.r[i], j.len);
+		memcpy(j.v[i], j.r[i], j.len);
+		or_synth_edits(seed + i, j.v[i], j.len, n_edits);
+	}
+	{   /* warm the reference's lazy CRC table before threads start */
+		uint8_t c[8];
+		delta_crc64_xz(j.r[0], 1, c);
+	}
+	double best = 1e30, sum = 0;
+	unsigned long long out_bytes = 0;
+	for (int rep = 0; rep < reps; rep++) {
+		j.next = 0;
+		j.out_bytes = 0;
+		pthread_mutex_init(&j.mu, NULL);
+		pthread_t *th = malloc(threads * sizeof(pthread_t));
+		double t0 = now();
+		for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, &j);
+		for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+		double dt = now() - t0;
+		free(th);
+		if (dt < best) best = dt;
+		sum += dt;
+		out_bytes = j.out_bytes;
+	}
+	double in_bytes = 2.0 * (double)j.len * (double)j.n_pairs;
+	printf("{\"pairs\": %zu, \"pair_len\": %zu, \"threads\": %d, \"reps\": %d, "
+	       "\"best_s\": %.6f, \"mean_s\": %.6f, \"in_bytes\": %.0f, "
+	       "\"out_bytes\": %llu, \"gib_per_s\": %.6f}\n",
+	       j.n_pairs, j.len, threads, reps, best, sum / reps, in_bytes,
+	       out_bytes, in_bytes / best / (1024.0 * 1024.0 * 1024.0));
+	return 0;
+}
+#endif
