@@ -1,0 +1,49 @@
+"""delta_compression_amd — MI355X-native batched delta codec (host mirror).
+
+Python view of the C ABI in ``include/delta_gpu.h`` (``lib/libdeltagpu.so``).
+Names and argument meanings follow the reference's interface for this path:
+
+* ``encode(R, V, algorithm, p, q)``  — ``delta encode`` (src/c/main.c:257-292;
+  src/python/delta.py:1579-1629): CRC-64/XZ of both buffers, onepass or
+  correcting differencing, placement, DLT\\x03 serialisation.
+* ``encode_batch(pairs, ...)``      — the same for many pairs at once.
+* ``EncodePlan``                    — device-resident batches (the hot path).
+* ``crc64_xz(data)``                — ``delta_crc64_xz`` (src/c/delta.h:294).
+* ``decode(R, delta)``              — ``delta decode`` (main.c:323-400).
+* ``info(delta)``                   — ``delta info`` (main.c:402-425).
+
+Everything runs on the GPU.  Importing this package without the built
+library, or calling it without a visible GPU, raises — there is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+from ._lib import (  # noqa: F401
+    ALGO_CORRECTING,
+    ALGO_GREEDY,
+    ALGO_ONEPASS,
+    BUF_CAP,
+    MAX_TABLE_SIZE,
+    SEED_LEN,
+    TABLE_SIZE,
+    Context,
+    DeltaError,
+    DiffOptions,
+    EncodePlan,
+    LIB_PATH,
+    crc64_xz,
+    decode,
+    default_context,
+    encode,
+    encode_batch,
+    info,
+    lib,
+    status_string,
+)
+
+__all__ = [
+    "ALGO_ONEPASS", "ALGO_CORRECTING", "ALGO_GREEDY", "SEED_LEN", "TABLE_SIZE",
+    "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan",
+    "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
+    "status_string", "LIB_PATH",
+]

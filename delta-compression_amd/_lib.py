@@ -1,0 +1,333 @@
+"""ctypes binding of libdeltagpu.so (include/delta_gpu.h).
+
+Device buffers are passed as integer device addresses (e.g. a torch tensor's
+``data_ptr()``) and streams as integer ``hipStream_t`` handles (e.g.
+``torch.cuda.current_stream().cuda_stream``).  No torch type crosses the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libdeltagpu.so")
+
+ALGO_GREEDY, ALGO_ONEPASS, ALGO_CORRECTING = 0, 1, 2
+SEED_LEN = 16
+TABLE_SIZE = 1048573
+MAX_TABLE_SIZE = 1073741827
+BUF_CAP = 256
+OPT_VERBOSE, OPT_SPLAY, OPT_INPLACE = 0, 1, 2
+
+_ALGOS = {"greedy": ALGO_GREEDY, "onepass": ALGO_ONEPASS, "correcting": ALGO_CORRECTING}
+
+STATUS = {
+    0: "DG_OK", 1: "DG_ERR_INVALID_ARG", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_TOO_LARGE",
+    4: "DG_ERR_NO_DEVICE", 5: "DG_ERR_HIP", 6: "DG_ERR_NOMEM", 7: "DG_ERR_CAPACITY",
+    8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC",
+}
+
+
+class DeltaError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{STATUS.get(code, code)}: {msg}" if msg else STATUS.get(code, str(code)))
+
+
+class DiffOptions(C.Structure):
+    """delta_diff_options_t (src/c/delta.h:248-257)."""
+    _fields_ = [("p", C.c_size_t), ("q", C.c_size_t), ("buf_cap", C.c_size_t),
+                ("max_table", C.c_size_t), ("flags", C.c_uint64)]
+
+    @classmethod
+    def make(cls, p: int = SEED_LEN, q: int = TABLE_SIZE, buf_cap: int = BUF_CAP,
+             max_table: int = MAX_TABLE_SIZE, flags: int = 0) -> "DiffOptions":
+        return cls(p, q, buf_cap, max_table, flags)
+
+
+class Buffer(C.Structure):
+    _fields_ = [("data", C.POINTER(C.c_uint8)), ("len", C.c_size_t)]
+
+
+class Pair(C.Structure):
+    _fields_ = [("r_off", C.c_uint64), ("r_len", C.c_uint64),
+                ("v_off", C.c_uint64), ("v_len", C.c_uint64)]
+
+
+class Span(C.Structure):
+    _fields_ = [("off", C.c_uint64), ("len", C.c_uint64)]
+
+
+class DecodeDesc(C.Structure):
+    _fields_ = [("ref_off", C.c_uint64), ("ref_len", C.c_uint64),
+                ("delta_off", C.c_uint64), ("delta_len", C.c_uint64),
+                ("out_off", C.c_uint64), ("out_cap", C.c_uint64)]
+
+
+class DeltaInfo(C.Structure):
+    _fields_ = [("inplace", C.c_int), ("version_size", C.c_uint64),
+                ("src_crc", C.c_uint8 * 8), ("dst_crc", C.c_uint8 * 8),
+                ("num_commands", C.c_uint64), ("num_copies", C.c_uint64),
+                ("num_adds", C.c_uint64), ("copy_bytes", C.c_uint64),
+                ("add_bytes", C.c_uint64)]
+
+
+def _share_torch_runtime() -> None:
+    """One HIP runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64/libhsa-runtime64.  If libdeltagpu.so
+    were loaded first it would bind /opt/rocm's runtime and torch would then
+    load a second one, which cannot open the device again ("No HIP GPUs are
+    available").  Importing torch first makes the dynamic linker satisfy our
+    libamdhip64.so.7 dependency with torch's already-loaded copy, so device
+    pointers and streams are shared by construction.
+    """
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch absent: /opt/rocm's runtime is used
+        pass
+
+
+def _load() -> C.CDLL:
+    _share_torch_runtime()
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C delta-compression_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u8p, sz, u32, u64, i32 = C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32
+    sig = {
+        "dg_abi_version": (C.c_int, []),
+        "dg_diff_options_default": (None, [C.POINTER(DiffOptions)]),
+        "dg_buffer_free": (None, [C.POINTER(Buffer)]),
+        "dg_context_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "dg_context_destroy": (None, [vp]),
+        "dg_context_stream": (vp, [vp]),
+        "dg_status_string": (C.c_char_p, [C.c_int]),
+        "dg_last_error": (C.c_char_p, [vp]),
+        "dg_encode_plan_create": (C.c_int, [vp, C.c_int, C.POINTER(Pair), u32, C.POINTER(DiffOptions), C.POINTER(vp)]),
+        "dg_encode_plan_output_bound": (u64, [vp]),
+        "dg_encode_plan_num_pairs": (u32, [vp]),
+        "dg_encode_plan_table_size": (u64, [vp, u32]),
+        "dg_encode_plan_run": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
+        "dg_encode_plan_set_timing": (C.c_int, [vp, C.c_int]),
+        "dg_encode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
+        "dg_encode_plan_copy_counts_device": (vp, [vp]),
+        "dg_encode_plan_destroy": (None, [vp]),
+        "dg_encode": (C.c_int, [vp, C.c_int, u8p, sz, u8p, sz, C.POINTER(DiffOptions), C.POINTER(Buffer)]),
+        "dg_encode_batch": (C.c_int, [vp, C.c_int, C.POINTER(u8p), C.POINTER(sz), C.POINTER(u8p),
+                                      C.POINTER(sz), u32, C.POINTER(DiffOptions), C.POINTER(Buffer),
+                                      C.POINTER(i32)]),
+        "dg_crc64_xz": (C.c_int, [vp, u8p, sz, C.c_uint8 * 8]),
+        "dg_crc64_xz_batch_device": (C.c_int, [vp, vp, C.POINTER(Span), u32, vp, vp]),
+        "dg_decode": (C.c_int, [vp, u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer)]),
+        "dg_decode_batch_device": (C.c_int, [vp, vp, vp, C.POINTER(DecodeDesc), u32, C.c_int, vp, vp, vp, vp]),
+        "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
+        "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def status_string(code: int) -> str:
+    return lib.dg_status_string(code).decode()
+
+
+def _u8(b: bytes):
+    return C.cast(C.c_char_p(b), C.POINTER(C.c_uint8)) if b else None
+
+
+def _opts(p=SEED_LEN, q=TABLE_SIZE, buf_cap=BUF_CAP, max_table=MAX_TABLE_SIZE, flags=0,
+          verbose=False, splay=False, inplace=False) -> DiffOptions:
+    f = flags | (verbose << OPT_VERBOSE) | (splay << OPT_SPLAY) | (inplace << OPT_INPLACE)
+    return DiffOptions.make(p, q, buf_cap, max_table, f)
+
+
+def _algo(a) -> int:
+    if isinstance(a, str):
+        if a not in _ALGOS:
+            raise ValueError(f"Unknown algorithm: {a}")
+        return _ALGOS[a]
+    return int(a)
+
+
+class Context:
+    """A HIP device + stream + constant tables (dg_context_t)."""
+
+    def __init__(self, device: int = -1):
+        h = C.c_void_p()
+        rc = lib.dg_context_create(device, C.byref(h))
+        if rc:
+            raise DeltaError(rc, "dg_context_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            lib.dg_context_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return lib.dg_context_stream(self.handle) or 0
+
+    def check(self, rc: int, what: str = ""):
+        if rc:
+            raise DeltaError(rc, f"{what}: {lib.dg_last_error(self.handle).decode()}")
+
+
+_default_ctx: Optional[Context] = None
+_ctx_lock = threading.Lock()
+
+
+def default_context() -> Context:
+    global _default_ctx
+    with _ctx_lock:
+        if _default_ctx is None:
+            _default_ctx = Context(-1)
+        return _default_ctx
+
+
+class EncodePlan:
+    """Device-resident batch (dg_encode_plan_t): fixed pair geometry + options.
+
+    ``pairs`` is a sequence of (r_off, r_len, v_off, v_len) into two device
+    arenas.  ``run`` takes device addresses and an optional stream handle.
+    """
+
+    def __init__(self, ctx: Context, algorithm, pairs: Sequence[Tuple[int, int, int, int]],
+                 **opt_kw):
+        self.ctx = ctx
+        n = len(pairs)
+        arr = (Pair * max(n, 1))(*[Pair(*p) for p in pairs])
+        o = _opts(**opt_kw)
+        h = C.c_void_p()
+        ctx.check(lib.dg_encode_plan_create(ctx.handle, _algo(algorithm), arr, n, C.byref(o),
+                                            C.byref(h)), "dg_encode_plan_create")
+        self.handle = h
+        self.n = n
+
+    @property
+    def output_bound(self) -> int:
+        return lib.dg_encode_plan_output_bound(self.handle)
+
+    def table_size(self, i: int) -> int:
+        return lib.dg_encode_plan_table_size(self.handle, i)
+
+    def set_timing(self, on: bool = True):
+        self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(on)), "set_timing")
+
+    def stage_times(self):
+        ms = (C.c_float * 8)()
+        names = (C.c_char_p * 8)()
+        k = lib.dg_encode_plan_stage_times(self.handle, ms, names, 8)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def copy_counts_ptr(self) -> int:
+        return lib.dg_encode_plan_copy_counts_device(self.handle) or 0
+
+    def run(self, d_ref: int, d_ver: int, d_out: int, out_cap: int, d_offsets: int,
+            d_status: int, stream: int = 0):
+        self.ctx.check(lib.dg_encode_plan_run(self.handle, d_ref, d_ver, d_out, out_cap, d_offsets,
+                                              d_status, stream or None), "dg_encode_plan_run")
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.dg_encode_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def encode(R: bytes, V: bytes, algorithm="onepass", p: int = SEED_LEN, q: int = TABLE_SIZE,
+           buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE, splay: bool = False,
+           inplace: bool = False, ctx: Optional[Context] = None) -> bytes:
+    """One pair, host bytes in, DLT\\x03 bytes out (src/c/main.c:257-292)."""
+    ctx = ctx or default_context()
+    out = Buffer()
+    o = _opts(p, q, buf_cap, max_table, splay=splay, inplace=inplace)
+    rc = lib.dg_encode(ctx.handle, _algo(algorithm), _u8(R), len(R), _u8(V), len(V), C.byref(o),
+                       C.byref(out))
+    ctx.check(rc, "dg_encode")
+    res = C.string_at(out.data, out.len)
+    lib.dg_buffer_free(C.byref(out))
+    return res
+
+
+def encode_batch(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: int = SEED_LEN,
+                 q: int = TABLE_SIZE, buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE,
+                 ctx: Optional[Context] = None) -> List[bytes]:
+    """Many pairs through the batched device path (host buffers in and out)."""
+    ctx = ctx or default_context()
+    n = len(pairs)
+    if n == 0:
+        return []
+    keep = [(bytes(r), bytes(v)) for r, v in pairs]
+    rp = (C.POINTER(C.c_uint8) * n)(*[_u8(r) for r, _ in keep])
+    vp = (C.POINTER(C.c_uint8) * n)(*[_u8(v) for _, v in keep])
+    rl = (C.c_size_t * n)(*[len(r) for r, _ in keep])
+    vl = (C.c_size_t * n)(*[len(v) for _, v in keep])
+    outs = (Buffer * n)()
+    st = (C.c_int32 * n)()
+    o = _opts(p, q, buf_cap, max_table)
+    ctx.check(lib.dg_encode_batch(ctx.handle, _algo(algorithm), rp, rl, vp, vl, n, C.byref(o), outs,
+                                  st), "dg_encode_batch")
+    res = []
+    for i in range(n):
+        if st[i]:
+            raise DeltaError(st[i], f"pair {i}")
+        res.append(C.string_at(outs[i].data, outs[i].len))
+        lib.dg_buffer_free(C.byref(outs[i]))
+    return res
+
+
+def crc64_xz(data: bytes, ctx: Optional[Context] = None) -> bytes:
+    """CRC-64/XZ, 8 bytes big-endian (src/c/delta.h:294-322), on the GPU."""
+    ctx = ctx or default_context()
+    out = (C.c_uint8 * 8)()
+    ctx.check(lib.dg_crc64_xz(ctx.handle, _u8(data), len(data), out), "dg_crc64_xz")
+    return bytes(out)
+
+
+def decode(R: bytes, delta: bytes, ignore_hash: bool = False,
+           ctx: Optional[Context] = None) -> bytes:
+    """Apply a delta to R on the GPU (src/c/main.c:323-400)."""
+    ctx = ctx or default_context()
+    out = Buffer()
+    rc = lib.dg_decode(ctx.handle, _u8(R), len(R), _u8(delta), len(delta), int(ignore_hash),
+                       C.byref(out))
+    ctx.check(rc, "dg_decode")
+    res = C.string_at(out.data, out.len) if out.len else b""
+    lib.dg_buffer_free(C.byref(out))
+    return res
+
+
+def info(delta: bytes) -> dict:
+    """Header and command summary (src/c/main.c:402-425)."""
+    d = DeltaInfo()
+    rc = lib.dg_delta_info(_u8(delta), len(delta), C.byref(d))
+    if rc:
+        raise DeltaError(rc, "dg_delta_info")
+    return {
+        "inplace": bool(d.inplace), "version_size": d.version_size,
+        "src_crc": bytes(d.src_crc), "dst_crc": bytes(d.dst_crc),
+        "num_commands": d.num_commands, "num_copies": d.num_copies, "num_adds": d.num_adds,
+        "copy_bytes": d.copy_bytes, "add_bytes": d.add_bytes,
+    }

@@ -1,0 +1,139 @@
+// dg_device.h — device-side data layout shared by the kernels and the host
+// plan code.  All structs are plain data (no pointers into host memory).
+#pragma once
+#include <stdint.h>
+
+namespace dg {
+
+constexpr uint64_t kMersenne = (1ULL << 61) - 1;   // src/c/delta.h:25
+constexpr uint64_t kBase = 263;                    // src/c/delta.h:24
+constexpr uint64_t kCrcPoly = 0xC96C5795D7870F42ULL;  // reflected, delta.h:303
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;        // "no slot" (q < 2^32 - 1)
+
+// CRC segmentation: one wave64 per segment, kCrcLaneBytes contiguous bytes per
+// lane.  Segments tile a span from its (16-byte aligned-up) end backwards.
+constexpr uint32_t kCrcLaneBytes = 1024;
+constexpr uint32_t kCrcSegBytes = 64 * kCrcLaneBytes;   // 64 KiB
+constexpr uint32_t kCrcWavesPerBlock = 4;
+
+// Onepass register history: chunks of 64 steps kept in VGPRs before the
+// epoch spills into a global (slot, tag) table.
+constexpr int kHistChunks = 8;
+
+struct PairDev {          // == dg_pair_t
+	uint64_t r_off, r_len, v_off, v_len;
+};
+
+struct PairPlanDev {
+	uint64_t q;            // table size for this pair (onepass.c:61-62)
+	uint64_t q_magic;      // floor((2^64-1)/q), Barrett
+	uint64_t rec_base;     // first record slot
+	uint32_t rec_cap;      // record capacity (>= #copies possible)
+	uint32_t pad;
+	// correcting only (correcting.c:116-136)
+	uint64_t f_size, f_magic;  // |F| and floor((2^64-1)/|F|)
+	uint64_t m, m_magic;       // checkpoint modulus and Barrett
+	uint64_t k;                // biased class (computed on device)
+};
+
+struct CrcSegDev {        // one wave's CRC segment
+	uint32_t span;         // span index
+	uint32_t j;            // segment index within the span (0 = first)
+};
+
+struct CrcSpanDev {
+	uint64_t off, len;     // byte range in the arena
+	uint32_t seg_base;     // first segment index
+	uint32_t nseg;         // number of segments (0 for len < 8)
+	uint32_t which;        // arena selector: 0 = reference arena, 1 = version arena
+	uint32_t pad;
+};
+
+// Precomputed GF(2) constants for the CRC combine steps, as nibble tables:
+// tab[c][16*j + n] = (n << 4j) * K_c mod P  (reflected), see dg_host.cpp.
+constexpr int kCrcLevels = 6;          // in-wave tree levels
+constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
+
+struct EncodeArgs {
+	const uint8_t* ref;
+	const uint8_t* ver;
+	const PairDev* pairs;
+	const PairPlanDev* pplan;
+	uint32_t n_pairs;
+	uint32_t p;
+	const uint64_t* powc;      // p constants: 263^(p-1-k) mod (2^61-1)
+	uint32_t* rec;             // 3 x u32 per COPY record (v, r, len)
+	uint32_t* n_rec;           // per pair
+	uint64_t* dsize;           // per pair serialized delta size
+	int32_t* status;           // per pair
+	// Tier-C table pool (long epochs)
+	unsigned long long* tables;   // n_tables x 2 x qmax entries
+	uint64_t qmax;
+	uint32_t n_tables;
+	uint32_t* table_locks;
+	uint32_t* table_tags;
+	// correcting
+	uint32_t buf_cap;
+	uint32_t* cand;            // correcting candidate scratch (per pair)
+};
+
+struct SerArgs {
+	const uint8_t* ver;
+	const PairDev* pairs;
+	const PairPlanDev* pplan;
+	const uint32_t* rec;
+	const uint32_t* n_rec;
+	const uint64_t* crc;       // 2 per pair: R, V
+	const uint64_t* offsets;   // n+1
+	uint8_t* out;
+	uint64_t out_cap;
+	int32_t* status;
+	uint32_t n_pairs;
+};
+
+struct CrcArgs {
+	const uint8_t* arena[2];   // selected by CrcSpanDev::which
+	const CrcSpanDev* spans;
+	const CrcSegDev* segs;
+	uint32_t n_segs;
+	uint32_t n_spans;
+	const uint64_t* tables;    // slice (8x256) + level nibble tables (6x256)
+	uint64_t* seg_crc;
+	uint64_t* out;             // per span: CRC-64/XZ value
+	const uint64_t* xinv;      // 16 constants x^(-8t) mod P
+	uint64_t kseg;             // x^(8*kCrcSegBytes) mod P
+};
+
+struct dg_decode_desc_dev {   // == dg_decode_desc_t
+	uint64_t ref_off, ref_len;
+	uint64_t delta_off, delta_len;
+	uint64_t out_off, out_cap;
+};
+
+struct DecodeArgs {
+	const uint8_t* ref;
+	const uint8_t* delta;
+	const dg_decode_desc_dev* descs;
+	uint32_t n;
+	int ignore_hash;
+	uint8_t* out;
+	uint64_t* out_len;
+	int32_t* status;
+	const uint64_t* ref_crc;   // CRC-64/XZ of each reference span
+};
+
+// launchers (dg_kernels.hip)
+#ifdef __HIP_PLATFORM_AMD__
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, hipStream_t st);
+hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
+hipError_t launch_serialize(const SerArgs& s, hipStream_t st);
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st);
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
+hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
+                                const uint64_t* out_crc, int32_t* status, hipStream_t st);
+hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
+                        uint64_t seed_base, uint64_t n_edits, hipStream_t st);
+#endif
+
+}  // namespace dg

@@ -1,0 +1,608 @@
+// dg_host.cpp — host side of libdeltagpu.so: the C ABI of include/delta_gpu.h.
+//
+// Thin by design: it sizes tables (onepass.c:61-62, correcting.c:116-129),
+// lays out device work buffers for a batch, launches the kernels of
+// dg_kernels.hip on one HIP stream, and moves host buffers through pinned
+// staging for the host-memory entry points.  There is no CPU compute
+// fallback: without a GPU every entry point fails with DG_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/delta_gpu.h"
+#include "dg_device.h"
+
+using namespace dg;
+
+// ───────────────────────────── small host math ────────────────────────────
+
+namespace {
+
+typedef unsigned __int128 u128;
+
+uint64_t mulmod64(uint64_t a, uint64_t b, uint64_t m) { return (uint64_t)((u128)a * b % m); }
+
+uint64_t powmod64(uint64_t b, uint64_t e, uint64_t m) {
+	uint64_t r = 1 % m;
+	b %= m;
+	for (; e; e >>= 1) {
+		if (e & 1) r = mulmod64(r, b, m);
+		b = mulmod64(b, b, m);
+	}
+	return r;
+}
+
+// Deterministic Miller-Rabin; the first 12 prime bases decide every n < 2^64.
+// (The reference uses 100 time-seeded random bases, src/c/hash.c:163-178.)
+bool is_prime_u64(uint64_t n) {
+	static const uint64_t B[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+	if (n < 2) return false;
+	for (uint64_t b : B) {
+		if (n == b) return true;
+		if (n % b == 0) return false;
+	}
+	uint64_t d = n - 1;
+	int s = 0;
+	while (!(d & 1)) { d >>= 1; ++s; }
+	for (uint64_t b : B) {
+		uint64_t x = powmod64(b, d, n);
+		if (x == 1 || x == n - 1) continue;
+		bool composite = true;
+		for (int i = 1; i < s && composite; ++i) {
+			x = mulmod64(x, x, n);
+			if (x == n - 1) composite = false;
+		}
+		if (composite) return false;
+	}
+	return true;
+}
+
+// src/c/hash.c:180-190
+uint64_t next_prime(uint64_t n) {
+	if (n <= 2) return 2;
+	uint64_t c = (n % 2 == 0) ? n + 1 : n;
+	while (!is_prime_u64(c)) c += 2;
+	return c;
+}
+
+// ── GF(2)[x] mod P, reflected representation (bit 63 = x^0) ──
+uint64_t gf2_mul(uint64_t a, uint64_t b) {
+	uint64_t p = 0;
+	for (int i = 0; i < 64; ++i) {
+		if ((a >> (63 - i)) & 1) p ^= b;
+		b = (b & 1) ? (b >> 1) ^ kCrcPoly : (b >> 1);
+	}
+	return p;
+}
+
+uint64_t gf2_xpow(uint64_t n) {   // x^n mod P
+	uint64_t r = 1ULL << 63, base = 1ULL << 62;
+	for (; n; n >>= 1) {
+		if (n & 1) r = gf2_mul(r, base);
+		base = gf2_mul(base, base);
+	}
+	return r;
+}
+
+uint64_t gf2_div_x(uint64_t z) {   // z * x^-1 mod P
+	const uint64_t l = z >> 63;   // bit 63 of z*... equals the lsb shifted out
+	return ((z ^ (l ? kCrcPoly : 0)) << 1) | l;
+}
+
+}  // namespace
+
+// ───────────────────────────── context ────────────────────────────────────
+
+struct dg_context {
+	int device = -1;
+	hipStream_t stream = nullptr;
+	uint64_t* d_crc_tables = nullptr;   // slice(8x256) + levels(6x256)
+	uint64_t* d_xinv = nullptr;         // 16
+	uint64_t kseg = 0;
+	std::string err;
+	// scratch reused by the host-buffer entry points
+	void* pin = nullptr;
+	size_t pin_cap = 0;
+};
+
+static int set_err(dg_context_t* ctx, int code, const char* fmt, ...) {
+	if (ctx) {
+		char buf[512];
+		va_list ap;
+		va_start(ap, fmt);
+		vsnprintf(buf, sizeof buf, fmt, ap);
+		va_end(ap);
+		ctx->err = buf;
+	}
+	return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                   \
+	do {                                                                                    \
+		hipError_t e_ = (expr);                                                             \
+		if (e_ != hipSuccess)                                                               \
+			return set_err((ctx), DG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+	} while (0)
+
+extern "C" {
+
+int dg_abi_version(void) { return DG_ABI_VERSION; }
+
+void dg_diff_options_default(dg_diff_options_t* o) {
+	o->p = DG_SEED_LEN;
+	o->q = DG_TABLE_SIZE;
+	o->buf_cap = DG_BUF_CAP;
+	o->max_table = DG_MAX_TABLE_SIZE;
+	o->flags = 0;
+}
+
+void dg_buffer_free(dg_buffer_t* b) {
+	if (!b) return;
+	free(b->data);
+	b->data = nullptr;
+	b->len = 0;
+}
+
+const char* dg_status_string(int s) {
+	switch (s) {
+	case DG_OK: return "ok";
+	case DG_ERR_INVALID_ARG: return "invalid argument";
+	case DG_ERR_UNSUPPORTED: return "unsupported option";
+	case DG_ERR_TOO_LARGE: return "input too large for the u32 delta format";
+	case DG_ERR_NO_DEVICE: return "no HIP device";
+	case DG_ERR_HIP: return "HIP runtime error";
+	case DG_ERR_NOMEM: return "out of memory";
+	case DG_ERR_CAPACITY: return "output buffer too small";
+	case DG_ERR_MALFORMED: return "malformed delta";
+	case DG_ERR_SRC_CRC: return "source file does not match delta";
+	case DG_ERR_DST_CRC: return "output integrity check failed";
+	default: return "unknown status";
+	}
+}
+
+const char* dg_last_error(const dg_context_t* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int dg_context_create(int device, dg_context_t** out) {
+	*out = nullptr;
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DG_ERR_NO_DEVICE;
+	dg_context_t* ctx = new (std::nothrow) dg_context_t();
+	if (!ctx) return DG_ERR_NOMEM;
+	if (device < 0) {
+		if (hipGetDevice(&device) != hipSuccess) device = 0;
+	}
+	if (device >= n) { delete ctx; return DG_ERR_NO_DEVICE; }
+	ctx->device = device;
+	if (hipSetDevice(device) != hipSuccess) { delete ctx; return DG_ERR_HIP; }
+	if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return DG_ERR_HIP; }
+
+	// CRC tables: slicing-by-8 and nibble tables of the combine constants
+	std::vector<uint64_t> tab(8 * 256 + kCrcLevels * kCrcNibTabWords);
+	for (int i = 0; i < 256; ++i) {
+		uint64_t c = (uint64_t)i;
+		for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+		tab[i] = c;
+	}
+	for (int k = 1; k < 8; ++k)
+		for (int i = 0; i < 256; ++i) {
+			const uint64_t prev = tab[(k - 1) * 256 + i];
+			tab[k * 256 + i] = (prev >> 8) ^ tab[prev & 0xff];
+		}
+	for (int lv = 0; lv < kCrcLevels; ++lv) {
+		const uint64_t K = gf2_xpow(8ull * kCrcLaneBytes << lv);
+		for (int j = 0; j < 16; ++j)
+			for (int nb = 0; nb < 16; ++nb)
+				tab[8 * 256 + lv * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
+	}
+	uint64_t xinv[16];
+	xinv[0] = 1ULL << 63;
+	for (int t = 1; t < 16; ++t) {
+		uint64_t z = xinv[t - 1];
+		for (int b = 0; b < 8; ++b) z = gf2_div_x(z);
+		xinv[t] = z;
+	}
+	ctx->kseg = gf2_xpow(8ull * kCrcSegBytes);
+	if (hipMalloc(&ctx->d_crc_tables, tab.size() * 8) != hipSuccess ||
+	    hipMalloc(&ctx->d_xinv, sizeof xinv) != hipSuccess ||
+	    hipMemcpy(ctx->d_crc_tables, tab.data(), tab.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMemcpy(ctx->d_xinv, xinv, sizeof xinv, hipMemcpyHostToDevice) != hipSuccess) {
+		dg_context_destroy(ctx);
+		return DG_ERR_HIP;
+	}
+	*out = ctx;
+	return DG_OK;
+}
+
+void dg_context_destroy(dg_context_t* ctx) {
+	if (!ctx) return;
+	hipSetDevice(ctx->device);
+	if (ctx->stream) hipStreamSynchronize(ctx->stream);
+	hipFree(ctx->d_crc_tables);
+	hipFree(ctx->d_xinv);
+	if (ctx->pin) hipHostFree(ctx->pin);
+	if (ctx->stream) hipStreamDestroy(ctx->stream);
+	delete ctx;
+}
+
+void* dg_context_stream(dg_context_t* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+}  // extern "C"
+
+// ───────────────────────────── CRC planning ───────────────────────────────
+
+namespace {
+
+// Segment layout for spans whose device address is 16-byte aligned at
+// offset 0 of the arena (checked at run time): the padded domain is
+// [align_down(off,16), align_up(off+len,16)).
+void plan_crc_spans(const std::vector<dg_span_t>& spans, const std::vector<uint32_t>& which,
+                    std::vector<CrcSpanDev>& sd, std::vector<CrcSegDev>& seg) {
+	sd.resize(spans.size());
+	seg.clear();
+	for (size_t i = 0; i < spans.size(); ++i) {
+		CrcSpanDev& s = sd[i];
+		s.off = spans[i].off;
+		s.len = spans[i].len;
+		s.seg_base = (uint32_t)seg.size();
+		s.nseg = 0;
+		s.which = which[i];
+		s.pad = 0;
+		if (s.len >= 8) {
+			const uint64_t a0 = s.off & ~15ull, a1 = (s.off + s.len + 15) & ~15ull;
+			s.nseg = (uint32_t)((a1 - a0 + kCrcSegBytes - 1) / kCrcSegBytes);
+			for (uint32_t j = 0; j < s.nseg; ++j) seg.push_back(CrcSegDev{(uint32_t)i, j});
+		}
+	}
+}
+
+struct DevBuf {
+	void* p = nullptr;
+	size_t n = 0;
+	~DevBuf() { if (p) hipFree(p); }
+	int alloc(size_t bytes) {
+		if (p) { hipFree(p); p = nullptr; }
+		n = bytes;
+		if (bytes == 0) return 0;
+		return hipMalloc(&p, bytes) == hipSuccess ? 0 : -1;
+	}
+	template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+// ───────────────────────────── encode plan ────────────────────────────────
+
+struct dg_encode_plan {
+	dg_context_t* ctx = nullptr;
+	dg_algorithm_t algo = DG_ALGO_ONEPASS;
+	dg_diff_options_t opts{};
+	uint32_t n = 0;
+	std::vector<dg_pair_t> pairs;
+	std::vector<PairPlanDev> pp;
+	uint64_t out_bound = 0;
+	uint64_t total_rec = 0;
+	uint64_t qmax = 0;
+	uint32_t n_tables = 0;
+	// device buffers
+	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_cand;
+	uint32_t n_crc_spans = 0, n_crc_segs = 0;
+	// timing
+	bool timing = false;
+	hipEvent_t ev[8] = {};
+	float stage_ms[8] = {};
+	int n_stages = 0;
+};
+
+static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize"};
+
+extern "C" {
+
+int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_t* pairs,
+                          uint32_t n, const dg_diff_options_t* opts, dg_encode_plan_t** out) {
+	*out = nullptr;
+	if (!ctx) return DG_ERR_INVALID_ARG;
+	dg_diff_options_t o;
+	if (opts) o = *opts; else dg_diff_options_default(&o);
+	if (algo == DG_ALGO_GREEDY)
+		return set_err(ctx, DG_ERR_UNSUPPORTED, "greedy is not implemented on the GPU path");
+	if (algo != DG_ALGO_ONEPASS && algo != DG_ALGO_CORRECTING)
+		return set_err(ctx, DG_ERR_INVALID_ARG, "unknown algorithm %d", (int)algo);
+	if ((o.flags >> DG_OPT_SPLAY) & 1)
+		return set_err(ctx, DG_ERR_UNSUPPORTED, "--splay is not supported (hash-table path only)");
+	if ((o.flags >> DG_OPT_INPLACE) & 1)
+		return set_err(ctx, DG_ERR_UNSUPPORTED, "in-place encode is not supported by the batch path");
+	if (o.p == 0) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len must be >= 1");
+	if (o.p > 65536) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len above 65536 is not supported");
+	if (n > 0 && !pairs) return DG_ERR_INVALID_ARG;
+
+	dg_encode_plan_t* P = new (std::nothrow) dg_encode_plan_t();
+	if (!P) return DG_ERR_NOMEM;
+	P->ctx = ctx;
+	P->algo = algo;
+	P->opts = o;
+	P->n = n;
+	P->pairs.assign(pairs, pairs + n);
+	P->pp.resize(n);
+	hipSetDevice(ctx->device);
+
+	std::map<uint64_t, uint64_t> qcache;
+	uint64_t rec = 0, bound = 0;
+	const uint64_t p = o.p;
+	for (uint32_t i = 0; i < n; ++i) {
+		const dg_pair_t& d = pairs[i];
+		if (d.r_len >= (1ull << 32) || d.v_len >= (1ull << 32)) {
+			delete P;
+			return set_err(ctx, DG_ERR_TOO_LARGE, "pair %u: buffers of 4 GiB or more do not fit the u32 format", i);
+		}
+		PairPlanDev& x = P->pp[i];
+		memset(&x, 0, sizeof x);
+		const uint64_t seeds = d.r_len >= p ? d.r_len - p + 1 : 0;
+		if (algo == DG_ALGO_ONEPASS) {
+			const uint64_t want = std::max<uint64_t>(o.q, seeds / p);   // onepass.c:61-62
+			auto it = qcache.find(want);
+			x.q = it != qcache.end() ? it->second : (qcache[want] = next_prime(want));
+		} else {
+			// correcting.c:116-129
+			const uint64_t mt = o.max_table > 0 ? o.max_table : DG_MAX_TABLE_SIZE;
+			uint64_t raw = seeds > 0 ? std::max<uint64_t>(o.q, 2 * seeds / p) : o.q;
+			raw = std::min<uint64_t>(raw, mt);
+			auto it = qcache.find(raw);
+			x.q = it != qcache.end() ? it->second : (qcache[raw] = next_prime(raw));
+			x.f_size = seeds > 0 ? next_prime(2 * seeds) : 1;
+			x.m = x.f_size <= x.q ? 1 : (x.f_size + x.q - 1) / x.q;
+			x.f_magic = UINT64_MAX / x.f_size;
+			x.m_magic = UINT64_MAX / x.m;
+		}
+		if (x.q >= 0xFFFFFFFFull) {
+			delete P;
+			return set_err(ctx, DG_ERR_TOO_LARGE, "table size %llu too large", (unsigned long long)x.q);
+		}
+		x.q_magic = UINT64_MAX / x.q;
+		x.rec_base = rec;
+		x.rec_cap = (uint32_t)(d.v_len / p + 1);
+		rec += x.rec_cap;
+		// delta <= 35 + |V| + (|V|/p) * max(0, 22 - p)   
+		bound += 35 + d.v_len + (d.v_len / p) * (p < 22 ? 22 - p : 0);
+		P->qmax = std::max<uint64_t>(P->qmax, x.q);
+	}
+	P->out_bound = bound;
+	P->total_rec = rec;
+
+	// constants 263^(p-1-k) mod (2^61-1)
+	std::vector<uint64_t> powc(p);
+	{
+		uint64_t c = 1;
+		for (uint64_t k = 0; k < p; ++k) {
+			powc[p - 1 - k] = c;
+			c = (uint64_t)((u128)c * kBase % kMersenne);
+		}
+	}
+	// CRC spans: 2 per pair (R then V); arena offsets are rebased at run time
+	std::vector<dg_span_t> spans(2ull * n);
+	std::vector<uint32_t> which(2ull * n);
+	for (uint32_t i = 0; i < n; ++i) {
+		spans[2ull * i] = dg_span_t{pairs[i].r_off, pairs[i].r_len};
+		spans[2ull * i + 1] = dg_span_t{pairs[i].v_off, pairs[i].v_len};
+		which[2ull * i] = 0;
+		which[2ull * i + 1] = 1;
+	}
+	std::vector<CrcSpanDev> sd;
+	std::vector<CrcSegDev> seg;
+	plan_crc_spans(spans, which, sd, seg);
+	P->n_crc_spans = (uint32_t)sd.size();
+	P->n_crc_segs = (uint32_t)seg.size();
+
+	// table-tier pool: 2 x qmax u64 per slot
+	const char* env = getenv("DG_TABLE_POOL_BYTES");
+	const uint64_t pool = env ? strtoull(env, nullptr, 0) : (1ull << 30);
+	const uint64_t per = 16ull * std::max<uint64_t>(P->qmax, 1);
+	P->n_tables = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(n, 1), pool / per));
+
+	int bad = 0;
+	bad |= P->d_pairs.alloc(sizeof(PairDev) * std::max<uint32_t>(n, 1));
+	bad |= P->d_pplan.alloc(sizeof(PairPlanDev) * std::max<uint32_t>(n, 1));
+	bad |= P->d_powc.alloc(8 * p);
+	bad |= P->d_rec.alloc(12 * std::max<uint64_t>(rec, 1));
+	bad |= P->d_nrec.alloc(4ull * std::max<uint32_t>(n, 1));
+	bad |= P->d_dsize.alloc(8ull * std::max<uint32_t>(n, 1));
+	bad |= P->d_crc_spans_r.alloc(sizeof(CrcSpanDev) * std::max<size_t>(sd.size(), 1));
+	bad |= P->d_crc_segs.alloc(sizeof(CrcSegDev) * std::max<size_t>(seg.size(), 1));
+	bad |= P->d_seg_crc.alloc(8 * std::max<size_t>(seg.size(), 1));
+	bad |= P->d_crc.alloc(8 * std::max<size_t>(sd.size(), 1));
+	bad |= P->d_tables.alloc(per * P->n_tables);
+	bad |= P->d_locks.alloc(4ull * P->n_tables);
+	bad |= P->d_tags.alloc(4ull * P->n_tables);
+	if (bad) {
+		delete P;
+		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
+	}
+	hipStream_t st = ctx->stream;
+	hipError_t e = hipSuccess;
+	if (n) {
+		e = hipMemcpyAsync(P->d_pairs.p, pairs, sizeof(PairDev) * n, hipMemcpyHostToDevice, st);
+		if (e == hipSuccess) e = hipMemcpyAsync(P->d_pplan.p, P->pp.data(), sizeof(PairPlanDev) * n, hipMemcpyHostToDevice, st);
+		if (e == hipSuccess) e = hipMemcpyAsync(P->d_crc_spans_r.p, sd.data(), sizeof(CrcSpanDev) * sd.size(), hipMemcpyHostToDevice, st);
+		if (e == hipSuccess && !seg.empty()) e = hipMemcpyAsync(P->d_crc_segs.p, seg.data(), sizeof(CrcSegDev) * seg.size(), hipMemcpyHostToDevice, st);
+	}
+	if (e == hipSuccess) e = hipMemcpyAsync(P->d_powc.p, powc.data(), 8 * p, hipMemcpyHostToDevice, st);
+	if (e == hipSuccess) e = hipMemsetAsync(P->d_tables.p, 0, P->d_tables.n, st);
+	if (e == hipSuccess) e = hipMemsetAsync(P->d_locks.p, 0, P->d_locks.n, st);
+	if (e == hipSuccess) e = hipMemsetAsync(P->d_tags.p, 0, P->d_tags.n, st);
+	if (e == hipSuccess) e = hipStreamSynchronize(st);
+	if (e != hipSuccess) {
+		delete P;
+		return set_err(ctx, DG_ERR_HIP, "plan upload failed: %s", hipGetErrorString(e));
+	}
+	*out = P;
+	return DG_OK;
+}
+
+uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t* P) { return P ? P->out_bound : 0; }
+uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t* P) { return P ? P->n : 0; }
+uint64_t dg_encode_plan_table_size(const dg_encode_plan_t* P, uint32_t i) {
+	return (P && i < P->n) ? P->pp[i].q : 0;
+}
+const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
+	return P ? P->d_nrec.as<uint32_t>() : nullptr;
+}
+
+int dg_encode_plan_set_timing(dg_encode_plan_t* P, int enable) {
+	if (!P) return DG_ERR_INVALID_ARG;
+	if (enable && !P->timing) {
+		for (int i = 0; i < 5; ++i)
+			if (hipEventCreate(&P->ev[i]) != hipSuccess) return DG_ERR_HIP;
+	}
+	P->timing = enable != 0;
+	return DG_OK;
+}
+
+int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
+	if (!P || !P->timing) return 0;
+	if (hipEventSynchronize(P->ev[4]) != hipSuccess) return 0;
+	int k = 0;
+	for (; k < 4 && k < n; ++k) {
+		float t = 0;
+		hipEventElapsedTime(&t, P->ev[k], P->ev[k + 1]);
+		if (ms) ms[k] = t;
+		if (names) names[k] = kStageNames[k];
+	}
+	return k;
+}
+
+int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t* d_ver,
+                       uint8_t* d_out, uint64_t out_cap, uint64_t* d_offsets, int32_t* d_status,
+                       void* stream) {
+	if (!P) return DG_ERR_INVALID_ARG;
+	dg_context_t* ctx = P->ctx;
+	if (P->n == 0) return DG_OK;
+	if (!d_ref || !d_ver || !d_out || !d_offsets || !d_status)
+		return set_err(ctx, DG_ERR_INVALID_ARG, "null device buffer");
+	if (((uintptr_t)d_ref & 15) || ((uintptr_t)d_ver & 15))
+		return set_err(ctx, DG_ERR_INVALID_ARG, "arena base pointers must be 16-byte aligned");
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[0], st));
+	// 1. CRC-64/XZ of every R (even spans) and V (odd spans)
+	{
+		CrcArgs a{};
+		a.arena[0] = d_ref;
+		a.arena[1] = d_ver;
+		a.spans = P->d_crc_spans_r.as<CrcSpanDev>();
+		a.segs = P->d_crc_segs.as<CrcSegDev>();
+		a.n_segs = P->n_crc_segs;
+		a.n_spans = P->n_crc_spans;
+		a.tables = ctx->d_crc_tables;
+		a.seg_crc = P->d_seg_crc.as<uint64_t>();
+		a.out = P->d_crc.as<uint64_t>();
+		a.xinv = ctx->d_xinv;
+		a.kseg = ctx->kseg;
+		HIPCHK(ctx, launch_crc(a, st));
+	}
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[1], st));
+	// 2. differencing -> COPY records + per-pair delta sizes
+	{
+		EncodeArgs a{};
+		a.ref = d_ref;
+		a.ver = d_ver;
+		a.pairs = P->d_pairs.as<PairDev>();
+		a.pplan = P->d_pplan.as<PairPlanDev>();
+		a.n_pairs = P->n;
+		a.p = (uint32_t)P->opts.p;
+		a.powc = P->d_powc.as<uint64_t>();
+		a.rec = P->d_rec.as<uint32_t>();
+		a.n_rec = P->d_nrec.as<uint32_t>();
+		a.dsize = P->d_dsize.as<uint64_t>();
+		a.status = d_status;
+		a.tables = P->d_tables.as<unsigned long long>();
+		a.qmax = P->qmax;
+		a.n_tables = P->n_tables;
+		a.table_locks = P->d_locks.as<uint32_t>();
+		a.table_tags = P->d_tags.as<uint32_t>();
+		a.buf_cap = (uint32_t)std::min<size_t>(P->opts.buf_cap, 1u << 20);
+		if (P->algo == DG_ALGO_ONEPASS)
+			HIPCHK(ctx, launch_onepass(a, a.p, st));
+		else
+			HIPCHK(ctx, launch_correcting(a, a.p, st));
+	}
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[2], st));
+	// 3. exclusive scan of sizes -> packed offsets
+	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[3], st));
+	// 4. serialise
+	{
+		SerArgs s{};
+		s.ver = d_ver;
+		s.pairs = P->d_pairs.as<PairDev>();
+		s.pplan = P->d_pplan.as<PairPlanDev>();
+		s.rec = P->d_rec.as<uint32_t>();
+		s.n_rec = P->d_nrec.as<uint32_t>();
+		s.crc = P->d_crc.as<uint64_t>();
+		s.offsets = d_offsets;
+		s.out = d_out;
+		s.out_cap = out_cap;
+		s.status = d_status;
+		s.n_pairs = P->n;
+		HIPCHK(ctx, launch_serialize(s, st));
+	}
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[4], st));
+	return DG_OK;
+}
+
+void dg_encode_plan_destroy(dg_encode_plan_t* P) {
+	if (!P) return;
+	hipSetDevice(P->ctx->device);
+	hipStreamSynchronize(P->ctx->stream);
+	for (auto& e : P->ev)
+		if (e) hipEventDestroy(e);
+	delete P;
+}
+
+}  // extern "C"
+
+// ───────────────────────────── CRC batch (utility) ────────────────────────
+
+extern "C" int dg_crc64_xz_batch_device(dg_context_t* ctx, const uint8_t* d_arena,
+                                        const dg_span_t* spans, uint32_t n, uint64_t* d_crc,
+                                        void* stream) {
+	if (!ctx || (n && (!d_arena || !spans || !d_crc))) return DG_ERR_INVALID_ARG;
+	if ((uintptr_t)d_arena & 15)
+		return set_err(ctx, DG_ERR_INVALID_ARG, "arena base pointer must be 16-byte aligned");
+	if (n == 0) return DG_OK;
+	hipSetDevice(ctx->device);
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+	std::vector<dg_span_t> sp(spans, spans + n);
+	std::vector<uint32_t> which(n, 0);
+	std::vector<CrcSpanDev> sd;
+	std::vector<CrcSegDev> seg;
+	plan_crc_spans(sp, which, sd, seg);
+	DevBuf d_sd, d_seg, d_segc;
+	if (d_sd.alloc(sizeof(CrcSpanDev) * sd.size()) || d_seg.alloc(sizeof(CrcSegDev) * std::max<size_t>(seg.size(), 1)) ||
+	    d_segc.alloc(8 * std::max<size_t>(seg.size(), 1)))
+		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
+	HIPCHK(ctx, hipMemcpyAsync(d_sd.p, sd.data(), sizeof(CrcSpanDev) * sd.size(), hipMemcpyHostToDevice, st));
+	if (!seg.empty())
+		HIPCHK(ctx, hipMemcpyAsync(d_seg.p, seg.data(), sizeof(CrcSegDev) * seg.size(), hipMemcpyHostToDevice, st));
+	CrcArgs a{};
+	a.arena[0] = a.arena[1] = d_arena;
+	a.spans = d_sd.as<CrcSpanDev>();
+	a.segs = d_seg.as<CrcSegDev>();
+	a.n_segs = (uint32_t)seg.size();
+	a.n_spans = n;
+	a.tables = ctx->d_crc_tables;
+	a.seg_crc = d_segc.as<uint64_t>();
+	a.out = d_crc;
+	a.xinv = ctx->d_xinv;
+	a.kseg = ctx->kseg;
+	HIPCHK(ctx, launch_crc(a, st));
+	HIPCHK(ctx, hipStreamSynchronize(st));   // the temporaries die here
+	return DG_OK;
+}

@@ -1,0 +1,281 @@
+// dg_host_io.cpp — host-memory entry points of libdeltagpu.so.
+//
+// These wrap the device-resident batch path (dg_encode_plan_*, the decode
+// kernels) with pinned staging and H2D/D2H copies, i.e. the end-to-end form
+// of the reference's CLI chain (src/c/main.c:249-292 encode, :335-385 decode).
+// The arithmetic always runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/delta_gpu.h"
+#include "dg_device.h"
+
+namespace {
+
+struct Dev {
+	void* p = nullptr;
+	~Dev() { if (p) hipFree(p); }
+	bool alloc(size_t n) { return hipMalloc(&p, n ? n : 16) == hipSuccess; }
+	template <class T> T* as() { return static_cast<T*>(p); }
+};
+
+struct Pinned {
+	void* p = nullptr;
+	~Pinned() { if (p) hipHostFree(p); }
+	bool alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault) == hipSuccess; }
+	template <class T> T* as() { return static_cast<T*>(p); }
+};
+
+uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
+
+uint32_t rd_u32be(const uint8_t* p) {
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_encode_batch(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* const* r,
+                    const size_t* r_len, const uint8_t* const* v, const size_t* v_len,
+                    uint32_t n, const dg_diff_options_t* opts, dg_buffer_t* outs,
+                    int32_t* status) {
+	if (!ctx || (n && (!r || !r_len || !v || !v_len || !outs))) return DG_ERR_INVALID_ARG;
+	for (uint32_t i = 0; i < n; ++i) outs[i].data = nullptr, outs[i].len = 0;
+	if (n == 0) return DG_OK;
+	hipStream_t st = (hipStream_t)dg_context_stream(ctx);
+
+	std::vector<dg_pair_t> pairs(n);
+	uint64_t rt = 0, vt = 0;
+	for (uint32_t i = 0; i < n; ++i) {
+		pairs[i] = dg_pair_t{rt, r_len[i], vt, v_len[i]};
+		rt += up16(r_len[i]);
+		vt += up16(v_len[i]);
+	}
+	dg_encode_plan_t* plan = nullptr;
+	int rc = dg_encode_plan_create(ctx, algo, pairs.data(), n, opts, &plan);
+	if (rc) return rc;
+	const uint64_t bound = dg_encode_plan_output_bound(plan);
+
+	Pinned h_in, h_off, h_st;
+	Dev d_ref, d_ver, d_out, d_off, d_st;
+	rc = DG_ERR_NOMEM;
+	if (!h_in.alloc(rt + vt) || !h_off.alloc(8ull * (n + 1)) || !h_st.alloc(4ull * n) ||
+	    !d_ref.alloc(rt) || !d_ver.alloc(vt) || !d_out.alloc(bound) ||
+	    !d_off.alloc(8ull * (n + 1)) || !d_st.alloc(4ull * n)) {
+		dg_encode_plan_destroy(plan);
+		return rc;
+	}
+	uint8_t* hr = h_in.as<uint8_t>();
+	uint8_t* hv = hr + rt;
+	for (uint32_t i = 0; i < n; ++i) {
+		if (r_len[i]) memcpy(hr + pairs[i].r_off, r[i], r_len[i]);
+		if (v_len[i]) memcpy(hv + pairs[i].v_off, v[i], v_len[i]);
+	}
+	rc = DG_ERR_HIP;
+	if (hipMemcpyAsync(d_ref.p, hr, rt, hipMemcpyHostToDevice, st) != hipSuccess ||
+	    hipMemcpyAsync(d_ver.p, hv, vt, hipMemcpyHostToDevice, st) != hipSuccess) {
+		dg_encode_plan_destroy(plan);
+		return rc;
+	}
+	rc = dg_encode_plan_run(plan, d_ref.as<uint8_t>(), d_ver.as<uint8_t>(), d_out.as<uint8_t>(),
+	                        bound, d_off.as<uint64_t>(), d_st.as<int32_t>(), st);
+	if (rc) { dg_encode_plan_destroy(plan); return rc; }
+	if (hipMemcpyAsync(h_off.p, d_off.p, 8ull * (n + 1), hipMemcpyDeviceToHost, st) != hipSuccess ||
+	    hipMemcpyAsync(h_st.p, d_st.p, 4ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+	    hipStreamSynchronize(st) != hipSuccess) {
+		dg_encode_plan_destroy(plan);
+		return DG_ERR_HIP;
+	}
+	const uint64_t* off = h_off.as<uint64_t>();
+	const uint64_t total = off[n];
+	Pinned h_out;
+	if (!h_out.alloc(total) ||
+	    hipMemcpyAsync(h_out.p, d_out.p, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+	    hipStreamSynchronize(st) != hipSuccess) {
+		dg_encode_plan_destroy(plan);
+		return DG_ERR_HIP;
+	}
+	dg_encode_plan_destroy(plan);
+	int first_bad = DG_OK;
+	for (uint32_t i = 0; i < n; ++i) {
+		const int32_t s = h_st.as<int32_t>()[i];
+		if (status) status[i] = s;
+		if (s != DG_OK) {
+			if (!first_bad) first_bad = s;
+			continue;
+		}
+		const uint64_t len = off[i + 1] - off[i];
+		outs[i].data = (uint8_t*)malloc(len ? len : 1);
+		if (!outs[i].data) return DG_ERR_NOMEM;
+		memcpy(outs[i].data, h_out.as<uint8_t>() + off[i], len);
+		outs[i].len = len;
+	}
+	return status ? DG_OK : first_bad;
+}
+
+int dg_encode(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* r, size_t r_len,
+              const uint8_t* v, size_t v_len, const dg_diff_options_t* opts, dg_buffer_t* out) {
+	if (!out) return DG_ERR_INVALID_ARG;
+	int32_t st = 0;
+	int rc = dg_encode_batch(ctx, algo, &r, &r_len, &v, &v_len, 1, opts, out, &st);
+	return rc ? rc : st;
+}
+
+int dg_crc64_xz_batch_device(dg_context_t* ctx, const uint8_t* d_arena, const dg_span_t* spans,
+                             uint32_t n, uint64_t* d_crc, void* stream);
+
+int dg_crc64_xz(dg_context_t* ctx, const uint8_t* data, size_t len, uint8_t out[DG_CRC_SIZE]) {
+	if (!ctx || (len && !data) || !out) return DG_ERR_INVALID_ARG;
+	hipStream_t st = (hipStream_t)dg_context_stream(ctx);
+	Dev d, c;
+	Pinned h;
+	if (!d.alloc(len) || !c.alloc(8) || !h.alloc(8)) return DG_ERR_NOMEM;
+	if (len && hipMemcpyAsync(d.p, data, len, hipMemcpyHostToDevice, st) != hipSuccess) return DG_ERR_HIP;
+	dg_span_t sp{0, len};
+	int rc = dg_crc64_xz_batch_device(ctx, d.as<uint8_t>(), &sp, 1, c.as<uint64_t>(), st);
+	if (rc) return rc;
+	if (hipMemcpyAsync(h.p, c.p, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+	    hipStreamSynchronize(st) != hipSuccess)
+		return DG_ERR_HIP;
+	const uint64_t v = *h.as<uint64_t>();
+	for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(v >> (56 - 8 * i));
+	return DG_OK;
+}
+
+int dg_delta_info(const uint8_t* d, size_t len, dg_delta_info_t* info) {
+	// src/c/encoding.c:111-178 walk, summary as delta_placed_summary (apply.c:98-115)
+	if (!d || !info) return DG_ERR_INVALID_ARG;
+	memset(info, 0, sizeof *info);
+	if (len < DG_HEADER_SIZE || memcmp(d, "DLT\x03", 4) != 0) return DG_ERR_MALFORMED;
+	info->inplace = d[4] & 1;
+	info->version_size = rd_u32be(d + 5);
+	memcpy(info->src_crc, d + 9, 8);
+	memcpy(info->dst_crc, d + 17, 8);
+	size_t pos = DG_HEADER_SIZE;
+	while (pos < len) {
+		const uint8_t t = d[pos++];
+		if (t == 0) return DG_OK;
+		if (t == 1) {
+			if (pos + 12 > len) return DG_ERR_MALFORMED;
+			info->num_copies++;
+			info->copy_bytes += rd_u32be(d + pos + 8);
+			pos += 12;
+		} else if (t == 2) {
+			if (pos + 8 > len) return DG_ERR_MALFORMED;
+			const uint32_t l = rd_u32be(d + pos + 4);
+			pos += 8;
+			if (pos + l > len) return DG_ERR_MALFORMED;
+			info->num_adds++;
+			info->add_bytes += l;
+			pos += l;
+		} else {
+			return DG_ERR_MALFORMED;
+		}
+		info->num_commands++;
+	}
+	return DG_OK;
+}
+
+int dg_synth_edit_pairs_device(dg_context_t* ctx, uint8_t* d_ref, uint8_t* d_ver, uint32_t n,
+                               uint64_t pair_len, uint64_t seed_base, uint64_t n_edits,
+                               void* stream) {
+	if (!ctx || (n && (!d_ref || !d_ver))) return DG_ERR_INVALID_ARG;
+	hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)dg_context_stream(ctx);
+	return dg::launch_synth(d_ref, d_ver, n, pair_len, seed_base, n_edits, st) == hipSuccess
+	           ? DG_OK
+	           : DG_ERR_HIP;
+}
+
+}  // extern "C"
+
+// ───────────────────────────── decode ─────────────────────────────────────
+
+extern "C" int dg_decode_batch_device(dg_context_t* ctx, const uint8_t* d_ref,
+                                      const uint8_t* d_delta, const dg_decode_desc_t* descs,
+                                      uint32_t n, int ignore_hash, uint8_t* d_out,
+                                      uint64_t* d_out_len, int32_t* d_status, void* stream) {
+	if (!ctx || (n && (!d_ref || !d_delta || !descs || !d_out || !d_out_len || !d_status)))
+		return DG_ERR_INVALID_ARG;
+	if (n == 0) return DG_OK;
+	if (((uintptr_t)d_ref & 15) || ((uintptr_t)d_out & 15)) return DG_ERR_INVALID_ARG;
+	hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)dg_context_stream(ctx);
+	Dev d_desc, d_rcrc, d_ocrc;
+	if (!d_desc.alloc(sizeof(dg_decode_desc_t) * n) || !d_rcrc.alloc(8ull * n) || !d_ocrc.alloc(8ull * n))
+		return DG_ERR_NOMEM;
+	if (hipMemcpyAsync(d_desc.p, descs, sizeof(dg_decode_desc_t) * n, hipMemcpyHostToDevice, st) != hipSuccess)
+		return DG_ERR_HIP;
+	// 1. CRC of every reference span (main.c:341-356)
+	if (!ignore_hash) {
+		std::vector<dg_span_t> sp(n);
+		for (uint32_t i = 0; i < n; ++i) sp[i] = dg_span_t{descs[i].ref_off, descs[i].ref_len};
+		int rc = dg_crc64_xz_batch_device(ctx, d_ref, sp.data(), n, d_rcrc.as<uint64_t>(), st);
+		if (rc) return rc;
+	}
+	// 2. parse + apply
+	dg::DecodeArgs a{};
+	a.ref = d_ref;
+	a.delta = d_delta;
+	a.descs = d_desc.as<dg::dg_decode_desc_dev>();
+	a.n = n;
+	a.ignore_hash = ignore_hash;
+	a.out = d_out;
+	a.out_len = d_out_len;
+	a.status = d_status;
+	a.ref_crc = d_rcrc.as<uint64_t>();
+	if (dg::launch_decode(a, st) != hipSuccess) return DG_ERR_HIP;
+	// 3. CRC of every output and the dst check (main.c:376-385)
+	if (!ignore_hash) {
+		std::vector<uint64_t> lens(n);
+		if (hipMemcpyAsync(lens.data(), d_out_len, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+		    hipStreamSynchronize(st) != hipSuccess)
+			return DG_ERR_HIP;
+		std::vector<dg_span_t> sp(n);
+		for (uint32_t i = 0; i < n; ++i) sp[i] = dg_span_t{descs[i].out_off, lens[i]};
+		int rc = dg_crc64_xz_batch_device(ctx, d_out, sp.data(), n, d_ocrc.as<uint64_t>(), st);
+		if (rc) return rc;
+		if (dg::launch_decode_verify(d_delta, a.descs, n, d_ocrc.as<uint64_t>(), d_status, st) != hipSuccess)
+			return DG_ERR_HIP;
+	}
+	return hipStreamSynchronize(st) == hipSuccess ? DG_OK : DG_ERR_HIP;
+}
+
+extern "C" int dg_decode(dg_context_t* ctx, const uint8_t* r, size_t r_len, const uint8_t* delta,
+                         size_t delta_len, int ignore_hash, dg_buffer_t* out) {
+	if (!ctx || !out || (r_len && !r) || (delta_len && !delta)) return DG_ERR_INVALID_ARG;
+	out->data = nullptr;
+	out->len = 0;
+	dg_delta_info_t inf;
+	if (delta_len < DG_HEADER_SIZE || memcmp(delta, "DLT\x03", 4) != 0) return DG_ERR_MALFORMED;
+	const uint64_t vsize = rd_u32be(delta + 5);
+	(void)inf;
+	const uint64_t cap = std::max<uint64_t>(vsize, r_len);
+	hipStream_t st = (hipStream_t)dg_context_stream(ctx);
+	Dev d_r, d_d, d_o, d_len, d_st;
+	Pinned h_o;
+	if (!d_r.alloc(r_len) || !d_d.alloc(delta_len) || !d_o.alloc(cap) || !d_len.alloc(8) ||
+	    !d_st.alloc(4) || !h_o.alloc(vsize))
+		return DG_ERR_NOMEM;
+	if ((r_len && hipMemcpyAsync(d_r.p, r, r_len, hipMemcpyHostToDevice, st) != hipSuccess) ||
+	    hipMemcpyAsync(d_d.p, delta, delta_len, hipMemcpyHostToDevice, st) != hipSuccess)
+		return DG_ERR_HIP;
+	dg_decode_desc_t desc{0, r_len, 0, delta_len, 0, cap};
+	int rc = dg_decode_batch_device(ctx, d_r.as<uint8_t>(), d_d.as<uint8_t>(), &desc, 1, ignore_hash,
+	                                d_o.as<uint8_t>(), d_len.as<uint64_t>(), d_st.as<int32_t>(), st);
+	if (rc) return rc;
+	int32_t s = 0;
+	if (hipMemcpy(&s, d_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return DG_ERR_HIP;
+	if (s) return s;
+	if (vsize && (hipMemcpyAsync(h_o.p, d_o.p, vsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
+	              hipStreamSynchronize(st) != hipSuccess))
+		return DG_ERR_HIP;
+	out->data = (uint8_t*)malloc(vsize ? vsize : 1);
+	if (!out->data) return DG_ERR_NOMEM;
+	if (vsize) memcpy(out->data, h_o.p, vsize);
+	out->len = vsize;
+	return DG_OK;
+}

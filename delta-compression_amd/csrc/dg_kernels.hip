@@ -1,0 +1,940 @@
+// dg_kernels.hip — CDNA4 (gfx950) kernels of the delta codec.
+//
+//   crc_segments_kernel / crc_finalize_kernel  CRC-64/XZ of every R and V
+//       (src/c/delta.h:294-322; main.c:259-260)
+//   onepass_kernel   one wave64 per pair, onepass differencing
+//       (src/c/onepass.c:32-297) in its epoch form
+//   scan_sizes_kernel  exclusive scan of per-pair delta sizes
+//   serialize_kernel   placement + DLT\x03 serialisation
+//       (src/c/apply.c:136-164, src/c/encoding.c:39-90)
+//   synth_*            synthetic batch generators (bench/test inputs)
+//
+// Written for wave64 / gfx950 only.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dg_device.h"
+
+namespace dg {
+
+// ───────────────────────────── common helpers ─────────────────────────────
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
+	return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ uint64_t mask_le(uint32_t j) {   // lanes 0..j
+	return j >= 63 ? ~0ULL : ((2ULL << j) - 1ULL);
+}
+
+__device__ __forceinline__ uint32_t ffs64(uint64_t m) {     // m != 0
+	return (uint32_t)__builtin_ctzll(m);
+}
+
+// x mod (2^61-1) for x < 2^63, canonical (src/c/hash.c:15-24).
+__device__ __forceinline__ uint64_t mod_m61(uint64_t x) {
+	uint64_t r = (x & kMersenne) + (x >> 61);
+	return r >= kMersenne ? r - kMersenne : r;
+}
+
+// x mod q by Barrett with magic = floor((2^64-1)/q).
+__device__ __forceinline__ uint64_t mod_q(uint64_t x, uint64_t q, uint64_t magic) {
+	uint64_t qh = __umul64hi(x, magic);
+	uint64_t r = x - qh * q;
+	if (r >= q) r -= q;
+	if (r >= q) r -= q;
+	return r;
+}
+
+// Karp-Rabin fingerprint of d[0..p) (src/c/hash.c:28-38) as a dot product
+// with the constants powc[k] = 263^(p-1-k) mod M: each term is an 8-bit x
+// 61-bit product, split into 32-bit halves so that both partial sums fit in
+// 64 bits; one fold at the end.
+template <int PF>
+__device__ __forceinline__ uint64_t window_fp(const uint8_t* d, uint32_t p,
+                                              const uint64_t* __restrict__ powc) {
+	uint64_t lo = 0, hi = 0;
+	if constexpr (PF > 0) {
+#pragma unroll
+		for (int k = 0; k < PF; ++k) {
+			const uint64_t c = powc[k];
+			const uint64_t b = d[k];
+			lo += b * (uint32_t)c;
+			hi += b * (uint32_t)(c >> 32);
+		}
+	} else {
+		for (uint32_t k = 0; k < p; ++k) {
+			const uint64_t c = powc[k];
+			const uint64_t b = d[k];
+			lo += b * (uint32_t)c;
+			hi += b * (uint32_t)(c >> 32);
+		}
+	}
+	// hi * 2^32 == (hi >> 29) * 2^61 + (hi & (2^29-1)) * 2^32 == (hi >> 29) + ...
+	const uint64_t t = lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29);
+	return mod_m61(t);
+}
+
+// Wave-parallel forward match extension (src/c/onepass.c:229-234): number of
+// equal leading bytes of a[] and b[], at most `limit`.  Uniform call.
+__device__ __noinline__ uint64_t extend_fwd(const uint8_t* a, const uint8_t* b,
+                                            uint64_t limit) {
+	const uint32_t lane = lane_id();
+	uint64_t ml = 0;
+	while (ml < limit) {
+		const uint64_t base = ml + 4ull * lane;
+		uint32_t bad = 4;
+#pragma unroll
+		for (int k = 3; k >= 0; --k) {
+			const uint64_t pos = base + k;
+			bool ok = false;
+			if (pos < limit) ok = a[pos] == b[pos];
+			if (!ok) bad = k;
+		}
+		const uint64_t m = __ballot(bad < 4);
+		if (m) {
+			const uint32_t f = ffs64(m);
+			return ml + 4ull * f + rdlane(bad, f);
+		}
+		ml += 256;
+	}
+	return limit;
+}
+
+// ───────────────────────────── onepass ────────────────────────────────────
+//
+// State between epochs is (v0, r0) only: every match bumps the table version
+// (onepass.c:263), so both tables are logically empty at an epoch start.
+// Step t of an epoch looks at V[v0+t..+p) and R[r0+t..+p).  Per step the
+// reference stores into HV/HR keeping the first writer of the version
+// (:141-166), then looks R's fingerprint up in HV, then V's in HR (:169-219).
+// So the candidate for lookup 1 at step t is the EARLIEST s <= t whose V-slot
+// equals R's slot at t; the match needs the bytes to agree (memcmp, :186);
+// equal bytes imply equal fingerprints, so the fingerprint test is only a
+// filter.
+//
+// Per epoch the wave evaluates 64 consecutive steps at once (lane = step):
+// fingerprints and slots in parallel, then walks the steps in order with
+// ballots over the slot history (register tier, up to kHistChunks chunks),
+// stopping at the first verified match.  Longer epochs move the history into
+// a per-pair (tag, step) table in HBM (table tier).
+
+struct TablePool {
+	unsigned long long* base;
+	uint64_t qmax;
+	uint32_t n;
+	uint32_t* locks;
+	uint32_t* tags;
+};
+
+__device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
+	return ((unsigned long long)tag << 32) | (0xFFFFFFFFu - rel);
+}
+
+__device__ __forceinline__ void tab_insert(unsigned long long* t, uint32_t slot,
+                                           uint32_t tag, uint32_t rel) {
+	if (slot != kSentinel)
+		__hip_atomic_fetch_max(t + slot, tab_key(tag, rel), __ATOMIC_RELAXED,
+		                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// earliest step stored in slot during this tag, or kSentinel
+__device__ __forceinline__ uint32_t tab_lookup(unsigned long long* t, uint32_t slot,
+                                               uint32_t tag, uint32_t max_rel) {
+	if (slot == kSentinel) return kSentinel;
+	// read at the memory side (an atomic no-op max): always coherent with the
+	// inserts above, whatever XCD last cached the line
+	unsigned long long e = __hip_atomic_fetch_max(t + slot, 0ull, __ATOMIC_RELAXED,
+	                                              __HIP_MEMORY_SCOPE_AGENT);
+	if ((uint32_t)(e >> 32) != tag) return kSentinel;
+	uint32_t rel = 0xFFFFFFFFu - (uint32_t)e;
+	return rel <= max_rel ? rel : kSentinel;
+}
+
+__device__ __forceinline__ void vm_drain() {
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int PF>
+__global__ __launch_bounds__(64) void onepass_kernel(EncodeArgs a) {
+	const uint32_t pair = blockIdx.x;
+	if (pair >= a.n_pairs) return;
+	const uint32_t lane = lane_id();
+	const PairDev pd = a.pairs[pair];
+	const PairPlanDev pp = a.pplan[pair];
+	const uint8_t* __restrict__ R = a.ref + pd.r_off;
+	const uint8_t* __restrict__ V = a.ver + pd.v_off;
+	const uint64_t rl = pd.r_len, vl = pd.v_len;
+	const uint32_t p = PF > 0 ? (uint32_t)PF : a.p;
+	const uint64_t q = pp.q, qmag = pp.q_magic;
+	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
+
+	uint32_t nrec = 0;
+	uint64_t dsz = 26;   // header (25) + END
+	int32_t st = 0;
+
+	// table tier state
+	int32_t tslot = -1;
+	uint32_t tag = 0;
+	unsigned long long* HV = nullptr;
+	unsigned long long* HR = nullptr;
+
+	uint64_t v0 = 0, r0 = 0;
+	bool scanning = vl > 0;
+	while (scanning) {
+		// early termination: no match is possible once either stream can no
+		// longer supply a window at the epoch start (onepass.c:102-104)
+		if (v0 + p > vl || r0 + p > rl) break;
+
+		uint32_t hsV[kHistChunks], hsR[kHistChunks], hfV[kHistChunks], hfR[kHistChunks];
+		bool matched = false;
+		bool in_table = false;
+		uint64_t vm = 0, rm = 0, ml = 0;
+
+		for (uint32_t c = 0; !matched; ++c) {
+			const uint64_t step = 64ull * c + lane;
+			const uint64_t vp = v0 + step, rp = r0 + step;
+			const bool cv = vp + p <= vl;
+			const bool cr = rp + p <= rl;
+			const uint64_t live = __ballot(cv || cr);
+			if (live == 0) { scanning = false; break; }   // both streams done
+			const uint32_t nlive = (uint32_t)__popcll(live);
+
+			uint64_t fV = 0, fR = 0;
+			uint32_t sV = kSentinel, sR = kSentinel;
+			if (cv) { fV = window_fp<PF>(V + vp, p, a.powc); sV = (uint32_t)mod_q(fV, q, qmag); }
+			if (cr) { fR = window_fp<PF>(R + rp, p, a.powc); sR = (uint32_t)mod_q(fR, q, qmag); }
+			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
+
+			if (c < (uint32_t)kHistChunks) {
+#pragma unroll
+				for (int k = 0; k < kHistChunks; ++k)
+					if ((uint32_t)k == c) { hsV[k] = sV; hsR[k] = sR; hfV[k] = fVl; hfR[k] = fRl; }
+
+				for (uint32_t j = 0; j < nlive && !matched; ++j) {
+					const uint64_t t = 64ull * c + j;
+					const bool ucr = r0 + t + p <= rl;
+					const bool ucv = v0 + t + p <= vl;
+					if (ucr) {
+						// lookup 1: R's slot at step t in the V history
+						const uint32_t x = rdlane(sR, j), xf = rdlane(fRl, j);
+						uint32_t s = kSentinel, sf = 0;
+#pragma unroll
+						for (int k = 0; k < kHistChunks; ++k) {
+							if (s == kSentinel && (uint32_t)k <= c) {
+								uint64_t m = __ballot(hsV[k] == x);
+								if ((uint32_t)k == c) m &= mask_le(j);
+								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfV[k], l); }
+							}
+						}
+						if (s != kSentinel && sf == xf) {
+							const uint64_t lim = min(vl - (v0 + s), rl - (r0 + t));
+							const uint64_t e = extend_fwd(V + v0 + s, R + r0 + t, lim);
+							if (e >= p) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; }
+						}
+					}
+					if (!matched && ucv) {
+						// lookup 2: V's slot at step t in the R history
+						const uint32_t x = rdlane(sV, j), xf = rdlane(fVl, j);
+						uint32_t s = kSentinel, sf = 0;
+#pragma unroll
+						for (int k = 0; k < kHistChunks; ++k) {
+							if (s == kSentinel && (uint32_t)k <= c) {
+								uint64_t m = __ballot(hsR[k] == x);
+								if ((uint32_t)k == c) m &= mask_le(j);
+								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfR[k], l); }
+							}
+						}
+						if (s != kSentinel && sf == xf) {
+							const uint64_t lim = min(vl - (v0 + t), rl - (r0 + s));
+							const uint64_t e = extend_fwd(V + v0 + t, R + r0 + s, lim);
+							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; }
+						}
+					}
+				}
+			} else {
+				// ── table tier: epoch longer than the register history ──
+				if (!in_table) {
+					in_table = true;
+					if (tslot < 0) {
+						// acquire a table from the pool (bounded spin)
+						uint32_t got = 0xFFFFFFFFu;
+						if (lane == 0) {
+							const uint32_t n = a.n_tables;
+							for (uint32_t it = 0; it < (1u << 26) && got == 0xFFFFFFFFu; ++it) {
+								const uint32_t sl = (pair + it) % n;
+								if (atomicCAS(&a.table_locks[sl], 0u, 1u) == 0u) got = sl;
+								else if ((it % n) == n - 1) __builtin_amdgcn_s_sleep(8);
+							}
+						}
+						got = rdlane(got, 0);
+						if (got == 0xFFFFFFFFu) { st = 5; scanning = false; break; }
+						tslot = (int32_t)got;
+						HV = a.tables + (uint64_t)got * 2ull * a.qmax;
+						HR = HV + a.qmax;
+						uint32_t t0 = 0;
+						if (lane == 0)
+							t0 = __hip_atomic_load(&a.table_tags[got], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						tag = rdlane(t0, 0);
+					}
+					if (tag == 0xFFFFFFFFu) {   // tag space exhausted: clear
+						for (uint64_t i = lane; i < 2ull * a.qmax; i += 64)
+							__hip_atomic_store(HV + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						vm_drain();
+						tag = 0;
+					}
+					++tag;
+#pragma unroll
+					for (int k = 0; k < kHistChunks; ++k) {
+						tab_insert(HV, hsV[k], tag, 64u * k + lane);
+						tab_insert(HR, hsR[k], tag, 64u * k + lane);
+					}
+				}
+				tab_insert(HV, sV, tag, (uint32_t)step);
+				tab_insert(HR, sR, tag, (uint32_t)step);
+				vm_drain();
+				const uint32_t c1 = cr ? tab_lookup(HV, sR, tag, (uint32_t)step) : kSentinel;
+				const uint32_t c2 = cv ? tab_lookup(HR, sV, tag, (uint32_t)step) : kSentinel;
+				const uint64_t any = __ballot(c1 != kSentinel || c2 != kSentinel);
+				if (any) {
+					for (uint32_t j = 0; j < nlive && !matched; ++j) {
+						if (!((any >> j) & 1)) continue;
+						const uint64_t t = 64ull * c + j;
+						const uint32_t s1 = rdlane(c1, j);
+						if (s1 != kSentinel) {
+							const uint64_t lim = min(vl - (v0 + s1), rl - (r0 + t));
+							const uint64_t e = extend_fwd(V + v0 + s1, R + r0 + t, lim);
+							if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; }
+						}
+						const uint32_t s2 = rdlane(c2, j);
+						if (!matched && s2 != kSentinel) {
+							const uint64_t lim = min(vl - (v0 + t), rl - (r0 + s2));
+							const uint64_t e = extend_fwd(V + v0 + t, R + r0 + s2, lim);
+							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; }
+						}
+					}
+				}
+			}
+		}
+		if (!matched) break;
+
+		// emit ADD (implicit gap) + COPY, then flush the tables (:243-263)
+		if (nrec >= pp.rec_cap) { st = 7; break; }
+		if (lane == 0) {
+			rec[3u * nrec + 0] = (uint32_t)vm;
+			rec[3u * nrec + 1] = (uint32_t)rm;
+			rec[3u * nrec + 2] = (uint32_t)ml;
+		}
+		++nrec;
+		dsz += 13 + (vm > v0 ? 9 + (vm - v0) : 0);
+		v0 = vm + ml;
+		r0 = rm + ml;
+	}
+	if (v0 < vl) dsz += 9 + (vl - v0);   // trailing ADD (:268-275)
+
+	if (tslot >= 0 && lane == 0) {
+		__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		vm_drain();
+		__hip_atomic_store(&a.table_locks[tslot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	if (lane == 0) {
+		a.n_rec[pair] = nrec;
+		a.dsize[pair] = dsz;
+		a.status[pair] = st;
+	}
+}
+
+template __global__ void onepass_kernel<16>(EncodeArgs);
+template __global__ void onepass_kernel<0>(EncodeArgs);
+
+// ───────────────────────────── scan of sizes ──────────────────────────────
+
+__global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __restrict__ sz,
+                                                          uint64_t* __restrict__ off,
+                                                          uint32_t n) {
+	__shared__ uint64_t buf[1024];
+	__shared__ uint64_t carry;
+	const uint32_t tid = threadIdx.x;
+	if (tid == 0) carry = 0;
+	__syncthreads();
+	for (uint32_t base = 0; base < n; base += 1024) {
+		const uint64_t x = base + tid < n ? sz[base + tid] : 0;
+		buf[tid] = x;
+		__syncthreads();
+		for (uint32_t d = 1; d < 1024; d <<= 1) {
+			const uint64_t y = tid >= d ? buf[tid - d] : 0;
+			__syncthreads();
+			buf[tid] += y;
+			__syncthreads();
+		}
+		const uint64_t c = carry;
+		if (base + tid < n) off[base + tid] = c + buf[tid] - x;
+		__syncthreads();
+		if (tid == 1023) carry = c + buf[1023];
+		__syncthreads();
+	}
+	if (tid == 0) off[n] = carry;
+}
+
+// ───────────────────────────── serialisation ──────────────────────────────
+
+__device__ __forceinline__ void put_u32be(uint8_t* o, uint32_t x) {
+	o[0] = (uint8_t)(x >> 24);
+	o[1] = (uint8_t)(x >> 16);
+	o[2] = (uint8_t)(x >> 8);
+	o[3] = (uint8_t)x;
+}
+
+
+
+// One 256-thread block per pair.  Commands are in V order with sequential
+// destinations (apply.c:136-164): every gap between consecutive COPYs is one
+// ADD of V bytes, so the COPY records alone describe the delta.
+__global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
+	const uint32_t pair = blockIdx.x;
+	const uint32_t tid = threadIdx.x;
+	__shared__ uint64_t scan[256];
+	__shared__ uint64_t big_dst[256], big_src[256], big_len[256];
+	__shared__ uint32_t n_big;
+	__shared__ uint64_t pos_sh;
+
+	const uint64_t base = s.offsets[pair];
+	const uint64_t end = s.offsets[pair + 1];
+	if (end > s.out_cap) {
+		if (tid == 0) s.status[pair] = 7;
+		return;
+	}
+	if (s.status[pair] != 0) return;
+	const PairDev pd = s.pairs[pair];
+	const PairPlanDev pp = s.pplan[pair];
+	const uint8_t* V = s.ver + pd.v_off;
+	const uint64_t vl = pd.v_len;
+	const uint32_t n = s.n_rec[pair];
+	const uint32_t* rec = s.rec + 3ull * pp.rec_base;
+	uint8_t* out = s.out + base;
+
+	if (tid == 0) {
+		out[0] = 'D'; out[1] = 'L'; out[2] = 'T'; out[3] = 3;
+		out[4] = 0;                       // standard delta
+		put_u32be(out + 5, (uint32_t)vl);
+		const uint64_t cs = s.crc[2ull * pair], cd = s.crc[2ull * pair + 1];
+		for (int i = 0; i < 8; ++i) {
+			out[9 + i] = (uint8_t)(cs >> (56 - 8 * i));
+			out[17 + i] = (uint8_t)(cd >> (56 - 8 * i));
+		}
+		pos_sh = 25;
+		n_big = 0;
+	}
+	__syncthreads();
+
+	for (uint32_t t0 = 0; t0 < n; t0 += 256) {
+		const uint32_t j = t0 + tid;
+		const bool valid = j < n;
+		uint32_t cv = 0, cr = 0, cl = 0;
+		uint64_t prev = 0;
+		if (valid) {
+			cv = rec[3u * j]; cr = rec[3u * j + 1]; cl = rec[3u * j + 2];
+			if (j > 0) prev = (uint64_t)rec[3u * (j - 1)] + rec[3u * (j - 1) + 2];
+		}
+		const uint64_t gap = valid ? cv - prev : 0;
+		const uint64_t sz = valid ? 13 + (gap ? 9 + gap : 0) : 0;
+		scan[tid] = sz;
+		__syncthreads();
+		for (uint32_t d = 1; d < 256; d <<= 1) {
+			const uint64_t y = tid >= d ? scan[tid - d] : 0;
+			__syncthreads();
+			scan[tid] += y;
+			__syncthreads();
+		}
+		const uint64_t pos = pos_sh;
+		if (valid) {
+			uint8_t* o = out + pos + scan[tid] - sz;
+			if (gap) {
+				o[0] = 2;
+				put_u32be(o + 1, (uint32_t)prev);
+				put_u32be(o + 5, (uint32_t)gap);
+				if (gap <= 64) {
+					for (uint64_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
+				} else {
+					const uint32_t b = atomicAdd(&n_big, 1u);
+					big_dst[b] = (uint64_t)(o + 9 - out);
+					big_src[b] = prev;
+					big_len[b] = gap;
+				}
+				o += 9 + gap;
+			}
+			o[0] = 1;
+			put_u32be(o + 1, cr);
+			put_u32be(o + 5, cv);
+			put_u32be(o + 9, cl);
+		}
+		__syncthreads();
+		const uint32_t nb = n_big;
+		for (uint32_t b = 0; b < nb; ++b) {
+			uint8_t* d = out + big_dst[b];
+			const uint8_t* src = V + big_src[b];
+			for (uint64_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
+		}
+		__syncthreads();
+		if (tid == 0) { pos_sh = pos + scan[255]; n_big = 0; }
+		__syncthreads();
+	}
+
+	uint64_t pos = pos_sh;
+	const uint64_t last = n ? (uint64_t)rec[3u * (n - 1)] + rec[3u * (n - 1) + 2] : 0;
+	if (last < vl) {   // trailing ADD
+		const uint64_t len = vl - last;
+		if (tid == 0) {
+			out[pos] = 2;
+			put_u32be(out + pos + 1, (uint32_t)last);
+			put_u32be(out + pos + 5, (uint32_t)len);
+		}
+		for (uint64_t i = tid; i < len; i += 256) out[pos + 9 + i] = V[last + i];
+		pos += 9 + len;
+	}
+	if (tid == 0) {
+		out[pos] = 0;   // END
+		if (pos + 1 != end - base) s.status[pair] = 5;   // size pass disagreed
+	}
+}
+
+// ───────────────────────────── CRC-64/XZ ──────────────────────────────────
+//
+// Tables (built on the host, uploaded once per context):
+//   slice[8][256]    slicing-by-8 tables of the reflected polynomial
+//   lvl[6][256]      nibble tables of "multiply by x^(8*L*2^l) mod P",
+//                    L = kCrcLaneBytes, for the in-wave combine tree
+// The raw CRC (init 0, no xorout) is linear, leading zero bytes are no-ops
+// and init = ~0 equals XOR-ing 0xFF into the first 8 data bytes, so each
+// lane hashes an equal-length chunk of a zero-front-padded span and the
+// chunks are combined as c_left * x^(8*len_right) ^ c_right.
+
+
+
+__device__ __forceinline__ uint64_t slice8(uint64_t x, const uint64_t* __restrict__ T) {
+	return T[7 * 256 + (x & 0xff)] ^ T[6 * 256 + ((x >> 8) & 0xff)] ^
+	       T[5 * 256 + ((x >> 16) & 0xff)] ^ T[4 * 256 + ((x >> 24) & 0xff)] ^
+	       T[3 * 256 + ((x >> 32) & 0xff)] ^ T[2 * 256 + ((x >> 40) & 0xff)] ^
+	       T[1 * 256 + ((x >> 48) & 0xff)] ^ T[0 * 256 + (x >> 56)];
+}
+
+__device__ __forceinline__ uint64_t mul_nib(uint64_t c, const uint64_t* __restrict__ tab) {
+	uint64_t r = 0;
+#pragma unroll
+	for (int j = 0; j < 16; ++j) r ^= tab[16 * j + ((c >> (4 * j)) & 15)];
+	return r;
+}
+
+// a * b mod P in the reflected representation (MSB = x^0), bit-serial.
+__device__ uint64_t gf2_mulmod(uint64_t a, uint64_t b) {
+	uint64_t p = 0;
+	for (int i = 0; i < 64; ++i) {
+		if ((a >> (63 - i)) & 1) p ^= b;
+		b = (b & 1) ? (b >> 1) ^ kCrcPoly : (b >> 1);
+	}
+	return p;
+}
+
+// keep-mask of bytes [lo, hi) within an 8-byte word (0 <= lo, hi <= 8)
+__device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
+	if (hi <= lo) return 0;
+	const uint64_t up = hi >= 8 ? ~0ULL : ((1ULL << (8 * hi)) - 1);
+	const uint64_t dn = lo <= 0 ? 0ULL : ((1ULL << (8 * lo)) - 1);
+	return up & ~dn;
+}
+
+__global__ __launch_bounds__(256) void crc_segments_kernel(CrcArgs a) {
+	__shared__ uint64_t T[8 * 256 + kCrcLevels * kCrcNibTabWords];
+	for (uint32_t i = threadIdx.x; i < 8 * 256 + kCrcLevels * kCrcNibTabWords; i += 256)
+		T[i] = a.tables[i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6;
+	const uint32_t lane = lane_id();
+	const uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave;
+	if (seg >= a.n_segs) return;
+	const CrcSegDev sd = a.segs[seg];
+	const CrcSpanDev sp = a.spans[sd.span];
+	const uintptr_t start = (uintptr_t)(a.arena[sp.which] + sp.off);
+	const uintptr_t end = start + sp.len;
+	const uintptr_t a0 = start & ~(uintptr_t)15;
+	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
+	const uintptr_t dom = a1 - (uintptr_t)sp.nseg * kCrcSegBytes;   // may wrap below a0
+	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
+
+	uint64_t reg = 0;
+	for (uint32_t w = 0; w < kCrcLaneBytes; w += 16) {
+		const uintptr_t addr = cs + w;
+		// words wholly before the data are virtual zeros: no-ops on a zero register
+		if ((intptr_t)(addr + 16 - a0) <= 0) continue;
+		const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(addr);
+		uint64_t lo = x.x, hi = x.y;
+		const int f = (int)((intptr_t)start - (intptr_t)addr);   // first data byte index
+		const int l = (int)((intptr_t)end - (intptr_t)addr);     // one past last
+		lo &= byte_mask(f, l);
+		hi &= byte_mask(f - 8, l - 8);
+		// init = ~0: invert the span's first 8 bytes
+		lo ^= byte_mask(f, f + 8);
+		hi ^= byte_mask(f - 8, f);
+		reg = slice8(reg ^ lo, T);
+		reg = slice8(reg ^ hi, T);
+	}
+	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
+	const uint64_t* L = T + 8 * 256;
+#pragma unroll
+	for (int lv = 0; lv < kCrcLevels; ++lv) {
+		const int d = 1 << lv;
+		const uint32_t plo = (uint32_t)__shfl_down((int)(uint32_t)reg, d, 64);
+		const uint32_t phi = (uint32_t)__shfl_down((int)(uint32_t)(reg >> 32), d, 64);
+		const uint64_t right = ((uint64_t)phi << 32) | plo;
+		const uint64_t shifted = mul_nib(reg, L + lv * kCrcNibTabWords);
+		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
+	}
+	if (lane == 0) a.seg_crc[seg] = reg;
+}
+
+__global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
+	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+	if (i >= a.n_spans) return;
+	const CrcSpanDev sp = a.spans[i];
+	uint64_t crc;
+	if (sp.len < 8) {
+		const uint8_t* d = a.arena[sp.which] + sp.off;
+		uint64_t c = ~0ULL;
+		for (uint64_t k = 0; k < sp.len; ++k) c = a.tables[(uint8_t)(c ^ d[k])] ^ (c >> 8);
+		crc = ~c;
+	} else {
+		uint64_t acc = 0;
+		for (uint32_t j = 0; j < sp.nseg; ++j)
+			acc = gf2_mulmod(a.kseg, acc) ^ a.seg_crc[sp.seg_base + j];
+		const uintptr_t end = (uintptr_t)(a.arena[sp.which] + sp.off) + sp.len;
+		const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
+		acc = gf2_mulmod(a.xinv[t], acc);   // undo the trailing pad bytes
+		crc = ~acc;
+	}
+	a.out[i] = crc;
+}
+
+// ───────────────────────────── synthetic inputs ───────────────────────────
+
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t k) {
+	uint64_t z = seed + k * 0x9E3779B97F4A7C15ULL;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+	return z ^ (z >> 31);
+}
+
+// R_i = splitmix64 bytes (seed_base + i); V_i = R_i (edits applied after)
+__global__ __launch_bounds__(256) void synth_random_kernel(uint8_t* ref, uint8_t* ver,
+                                                           uint64_t pair_len, uint64_t seed_base,
+                                                           uint64_t words_total) {
+	const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+	if (w >= words_total) return;
+	const uint64_t words_per_pair = (pair_len + 7) / 8;
+	const uint64_t pair = w / words_per_pair, k = w % words_per_pair;
+	const uint64_t val = splitmix_at(seed_base + pair, k + 1);
+	const uint64_t off = pair * pair_len + 8 * k;
+	if (8 * k + 8 <= pair_len) {
+		uint8_t* r = ref + off;
+		uint8_t* v = ver + off;
+		for (int b = 0; b < 8; ++b) { r[b] = (uint8_t)(val >> (8 * b)); v[b] = (uint8_t)(val >> (8 * b)); }
+	} else {
+		for (uint64_t b = 0; 8 * k + b < pair_len; ++b) {
+			ref[off + b] = (uint8_t)(val >> (8 * b));
+			ver[off + b] = (uint8_t)(val >> (8 * b));
+		}
+	}
+}
+
+__global__ __launch_bounds__(64) void synth_edits_kernel(uint8_t* ver, uint32_t n_pairs,
+                                                         uint64_t pair_len, uint64_t seed_base,
+                                                         uint64_t n_edits) {
+	const uint32_t pair = blockIdx.x * 64 + threadIdx.x;
+	if (pair >= n_pairs || pair_len == 0) return;
+	const uint64_t s = (seed_base + pair) ^ 0xD1B54A32D192ED03ULL;
+	uint8_t* v = ver + (uint64_t)pair * pair_len;
+	for (uint64_t e = 0; e < n_edits; ++e) {
+		const uint64_t pos = splitmix_at(s, 2 * e + 1) % pair_len;
+		v[pos] = (uint8_t)splitmix_at(s, 2 * e + 2);
+	}
+}
+
+}  // namespace dg
+
+// ───────────────────────────── launchers (C++ linkage, internal) ──────────
+
+namespace dg {
+
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, hipStream_t st) {
+	if (a.n_pairs == 0) return hipSuccess;
+	if (p == 16)
+		hipLaunchKernelGGL(onepass_kernel<16>, dim3(a.n_pairs), dim3(64), 0, st, a);
+	else
+		hipLaunchKernelGGL(onepass_kernel<0>, dim3(a.n_pairs), dim3(64), 0, st, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
+	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
+	return hipGetLastError();
+}
+
+hipError_t launch_serialize(const SerArgs& s, hipStream_t st) {
+	if (s.n_pairs == 0) return hipSuccess;
+	hipLaunchKernelGGL(serialize_kernel, dim3(s.n_pairs), dim3(256), 0, st, s);
+	return hipGetLastError();
+}
+
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st) {
+	if (a.n_segs)
+		hipLaunchKernelGGL(crc_segments_kernel,
+		                   dim3((a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock),
+		                   dim3(64 * kCrcWavesPerBlock), 0, st, a);
+	if (a.n_spans)
+		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
+                        uint64_t seed_base, uint64_t n_edits, hipStream_t st) {
+	const uint64_t words = (uint64_t)n_pairs * ((pair_len + 7) / 8);
+	if (words)
+		hipLaunchKernelGGL(synth_random_kernel, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st,
+		                   ref, ver, pair_len, seed_base, words);
+	if (n_edits && n_pairs)
+		hipLaunchKernelGGL(synth_edits_kernel, dim3((n_pairs + 63) / 64), dim3(64), 0, st, ver,
+		                   n_pairs, pair_len, seed_base, n_edits);
+	return hipGetLastError();
+}
+
+}  // namespace dg
+
+// ───────────────────────────── decode + apply ─────────────────────────────
+//
+// One wave per delta stream (src/c/encoding.c:111-178 parse,
+// src/c/apply.c:229-284 apply).  Lane 0 parses command headers out of an LDS
+// window of the stream; commands are applied in batches of up to 64, one per
+// lane, when no command of the batch touches bytes another one (earlier in
+// stream order) reads or writes; otherwise the batch is replayed strictly in
+// order with a wave-wide memmove per command.  Either way the result equals
+// the reference's sequential memcpy/memmove replay.  All offsets are bounds
+// checked (the reference does not check, apply.c:236-243).
+
+namespace dg {
+
+
+
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+	return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// wave-wide memmove of len bytes (src and dst may overlap)
+__device__ void wave_memmove(uint8_t* dst, const uint8_t* src, uint64_t len) {
+	const uint32_t lane = lane_id();
+	if (len == 0 || dst == src) return;
+	const bool backward = dst > src && dst < src + len;
+	const uint64_t chunk = 64 * 4;
+	const uint64_t nch = (len + chunk - 1) / chunk;
+	for (uint64_t c = 0; c < nch; ++c) {
+		const uint64_t cc = backward ? nch - 1 - c : c;
+		const uint64_t base = cc * chunk + 4ull * lane;
+		uint8_t b[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k) b[k] = base + k < len ? src[base + k] : 0;
+		// every lane's loads of this chunk complete before any store
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int k = 0; k < 4; ++k)
+			if (base + k < len) dst[base + k] = b[k];
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__builtin_amdgcn_wave_barrier();
+	}
+}
+
+__device__ __forceinline__ bool overlap(uint64_t a, uint64_t al, uint64_t b, uint64_t bl) {
+	return al && bl && a < b + bl && b < a + al;
+}
+
+constexpr uint32_t kDecWin = 2048;   // LDS window of the command stream
+
+__global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
+	const uint32_t i = blockIdx.x;
+	if (i >= a.n) return;
+	const uint32_t lane = lane_id();
+	__shared__ uint8_t win[kDecWin + 16];
+	__shared__ uint32_t c_kind[64];
+	__shared__ uint64_t c_src[64], c_dst[64], c_len[64];
+
+	const dg_decode_desc_dev dd = a.descs[i];
+	const uint8_t* D = a.delta + dd.delta_off;
+	const uint64_t dl = dd.delta_len;
+	const uint8_t* R = a.ref + dd.ref_off;
+	const uint64_t rl = dd.ref_len;
+	uint8_t* O = a.out + dd.out_off;
+
+	int32_t st = 0;
+	uint64_t vsize = 0;
+	if (dl < 25 || D[0] != 'D' || D[1] != 'L' || D[2] != 'T' || D[3] != 3) st = 8;
+	bool inplace = false;
+	if (!st) {
+		inplace = D[4] & 1;
+		vsize = be32(D + 5);
+		if (!a.ignore_hash) {
+			uint64_t sc = 0;
+			for (int k = 0; k < 8; ++k) sc = (sc << 8) | D[9 + k];
+			if (sc != a.ref_crc[i]) st = 9;
+		}
+	}
+	const uint64_t bsz = inplace ? max(rl, vsize) : vsize;
+	if (!st && bsz > dd.out_cap) st = 7;
+	if (st) {
+		if (lane == 0) { a.status[i] = st; a.out_len[i] = 0; }
+		return;
+	}
+	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
+	const uint64_t init = inplace ? rl : 0;
+	for (uint64_t k = lane; k < bsz; k += 64) O[k] = k < init ? R[k] : 0;
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__builtin_amdgcn_wave_barrier();
+
+	uint64_t pos = 25;          // next unparsed byte of the stream
+	uint64_t wbase = ~0ull;     // stream offset of win[0]
+	bool done = false;
+	while (!done && !st) {
+		// ── lane 0 parses up to 64 commands (LDS window refilled as needed) ──
+		uint32_t cnt = 0;
+		while (cnt < 64 && !done && !st) {
+			if (pos >= dl) { done = true; break; }   // missing END: end of input
+			if (wbase == ~0ull || pos < wbase || pos + 13 > wbase + kDecWin) {
+				wbase = pos;
+				__builtin_amdgcn_wave_barrier();
+				for (uint32_t k = lane; k < kDecWin; k += 64) win[k] = wbase + k < dl ? D[wbase + k] : 0;
+				__syncthreads();
+			}
+			const uint8_t* w = win + (pos - wbase);
+			const uint32_t t = w[0];
+			if (t == 0) { done = true; break; }
+			if (t == 1) {
+				if (pos + 13 > dl) { st = 8; break; }
+				if (lane == 0) {
+					c_kind[cnt] = 1;
+					c_src[cnt] = be32(w + 1);
+					c_dst[cnt] = be32(w + 5);
+					c_len[cnt] = be32(w + 9);
+				}
+				pos += 13;
+			} else if (t == 2) {
+				if (pos + 9 > dl) { st = 8; break; }
+				const uint64_t len = be32(w + 5);
+				if (pos + 9 + len > dl) { st = 8; break; }
+				if (lane == 0) {
+					c_kind[cnt] = 2;
+					c_src[cnt] = pos + 9;   // payload offset in the stream
+					c_dst[cnt] = be32(w + 1);
+					c_len[cnt] = len;
+				}
+				pos += 9 + len;
+			} else {
+				st = 8;
+				break;
+			}
+			++cnt;
+		}
+		__syncthreads();
+		if (st || cnt == 0) break;
+
+		// ── apply the batch ──
+		const bool mine = lane < cnt;
+		const uint32_t kind = mine ? c_kind[lane] : 0;
+		const uint64_t src = mine ? c_src[lane] : 0, dst = mine ? c_dst[lane] : 0, len = mine ? c_len[lane] : 0;
+		bool bad = false;
+		if (mine) {
+			if (dst + len > bsz) bad = true;
+			if (kind == 1 && src + len > (inplace ? bsz : rl)) bad = true;
+		}
+		if (__ballot(bad)) { st = 8; break; }
+		// conflicts with earlier commands of the batch (writes vs writes; and
+		// in-place: writes vs reads both ways)
+		bool conflict = false;
+		const bool reads_buf = inplace && kind == 1;
+		for (uint32_t k = 0; k + 1 < cnt; ++k) {
+			const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)src, k)) |
+			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(src >> 32), k) << 32);
+			const uint64_t kd = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)dst, k)) |
+			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(dst >> 32), k) << 32);
+			const uint64_t kl = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)len, k)) |
+			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(len >> 32), k) << 32);
+			const bool kreads = inplace && rdlane(kind, k) == 1;
+			if (mine && lane > k) {
+				if (overlap(kd, kl, dst, len)) conflict = true;
+				if (reads_buf && overlap(kd, kl, src, len)) conflict = true;
+				if (kreads && overlap(ks, kl, dst, len)) conflict = true;
+			}
+		}
+		if (__ballot(conflict) == 0) {
+			// independent: small commands by their own lane, large ones by the wave
+			const bool small = mine && len <= 64;
+			if (small && len) {
+				const uint8_t* s = kind == 1 ? (inplace ? O + src : R + src) : D + src;
+				uint8_t* d = O + dst;
+				if (d > s && d < s + len) {
+					for (uint64_t b = len; b-- > 0;) d[b] = s[b];
+				} else {
+					for (uint64_t b = 0; b < len; ++b) d[b] = s[b];
+				}
+			}
+			uint64_t big = __ballot(mine && !small);
+			while (big) {
+				const uint32_t k = ffs64(big);
+				big &= big - 1;
+				const uint32_t kk = rdlane(kind, k);
+				const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), k) << 32) | rdlane((uint32_t)src, k);
+				const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), k) << 32) | rdlane((uint32_t)dst, k);
+				const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), k) << 32) | rdlane((uint32_t)len, k);
+				wave_memmove(O + kd, kk == 1 ? (inplace ? O + ks : R + ks) : D + ks, kl);
+			}
+		} else {
+			// strict stream order (apply.c:257-266)
+			for (uint32_t k = 0; k < cnt; ++k) {
+				const uint32_t kk = c_kind[k];
+				wave_memmove(O + c_dst[k], kk == 1 ? (inplace ? O + c_src[k] : R + c_src[k]) : D + c_src[k], c_len[k]);
+			}
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+	}
+	if (lane == 0) {
+		a.status[i] = st;
+		a.out_len[i] = st ? 0 : vsize;
+	}
+}
+
+// dst CRC check after the output CRC pass (main.c:379-385)
+__global__ __launch_bounds__(64) void decode_verify_kernel(const uint8_t* delta,
+                                                           const dg_decode_desc_dev* descs,
+                                                           uint32_t n, const uint64_t* out_crc,
+                                                           int32_t* status) {
+	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+	if (i >= n || status[i] != 0) return;
+	const uint8_t* D = delta + descs[i].delta_off;
+	uint64_t dc = 0;
+	for (int k = 0; k < 8; ++k) dc = (dc << 8) | D[17 + k];
+	if (dc != out_crc[i]) status[i] = 10;
+}
+
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
+	if (a.n) hipLaunchKernelGGL(decode_kernel, dim3(a.n), dim3(64), 0, st, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
+                                const uint64_t* out_crc, int32_t* status, hipStream_t st) {
+	if (n) hipLaunchKernelGGL(decode_verify_kernel, dim3((n + 63) / 64), dim3(64), 0, st, delta, descs, n, out_crc, status);
+	return hipGetLastError();
+}
+
+hipError_t launch_correcting(const EncodeArgs&, uint32_t, hipStream_t) { return hipErrorNotSupported; }
+
+}  // namespace dg

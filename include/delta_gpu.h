@@ -1,0 +1,258 @@
+/*
+ * delta_gpu.h — C ABI of the MI355X-native delta codec (libdeltagpu.so).
+ *
+ * Drop-in boundary for the hot path of darrelllong/Delta-Compression:
+ *
+ *   reference chain (src/c/main.c:257-292)          this library
+ *   ---------------------------------------------   ---------------------------
+ *   delta_crc64_xz(R), delta_crc64_xz(V)            \
+ *     (src/c/delta.h:294-322)                        \
+ *   delta_diff(ALGO_ONEPASS|ALGO_CORRECTING, ...)     > dg_encode / dg_encode_batch /
+ *     (src/c/correcting.c:499-519 -> onepass.c:32,   /  dg_encode_plan_run
+ *      correcting.c:81)                             /
+ *   delta_place_commands (src/c/apply.c:136-164)   /
+ *   delta_encode(placed, false, |V|, src, dst)    /
+ *     (src/c/encoding.c:39-90)
+ *   delta_decode + delta_apply_placed(_inplace)     dg_decode / dg_decode_batch
+ *     + CRC checks (encoding.c:111-178,
+ *       apply.c:229-284, main.c:341-385)
+ *   delta_crc64_xz (delta.h:294)                    dg_crc64_xz / dg_crc64_xz_batch_device
+ *
+ * Output bytes are identical to the reference's `delta encode` at the same
+ * --seed-len / --table-size / --max-table (the DLT\x03 format of
+ * src/c/encoding.c:39-90, README.md:125-149).
+ *
+ * Differences from the reference contract (src/c/delta.h), by design:
+ *   - every call returns a dg_status_t instead of abort()/exit(1)
+ *     (delta.h:44-79, encoding.c:119-172);
+ *   - no per-command allocations: results are arenas with explicit frees;
+ *   - thread-safe: constant tables are built at context creation;
+ *   - DELTA_OPT_SPLAY (delta.h:222) and ALGO_GREEDY are rejected with
+ *     DG_ERR_UNSUPPORTED (splay changes correcting output; greedy is outside
+ *     the GPU hot path);
+ *   - inputs of 4 GiB or more are rejected (DG_ERR_TOO_LARGE): the format's
+ *     u32 fields would silently truncate them (encoding.c:63,72-78).
+ *
+ * All device pointers are plain HIP device pointers; `stream` is a
+ * hipStream_t passed as void* (NULL = the context's own stream).  No C++ or
+ * torch types cross this boundary.
+ */
+#ifndef DELTA_GPU_H
+#define DELTA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_ABI_VERSION 1
+
+/* Defaults mirror src/c/delta.h:21-35. */
+#define DG_SEED_LEN        16
+#define DG_TABLE_SIZE      1048573UL
+#define DG_MAX_TABLE_SIZE  1073741827UL
+#define DG_BUF_CAP         256
+#define DG_HEADER_SIZE     25
+#define DG_CRC_SIZE        8
+
+typedef enum {
+	DG_OK              = 0,
+	DG_ERR_INVALID_ARG = 1,
+	DG_ERR_UNSUPPORTED = 2,   /* greedy, --splay, --inplace encode */
+	DG_ERR_TOO_LARGE   = 3,   /* a buffer >= 4 GiB */
+	DG_ERR_NO_DEVICE   = 4,
+	DG_ERR_HIP         = 5,
+	DG_ERR_NOMEM       = 6,
+	DG_ERR_CAPACITY    = 7,   /* output arena too small */
+	DG_ERR_MALFORMED   = 8,   /* not a delta / truncated / bad command */
+	DG_ERR_SRC_CRC     = 9,   /* reference does not match src_crc */
+	DG_ERR_DST_CRC     = 10   /* reconstructed output does not match dst_crc */
+} dg_status_t;
+
+/* Numbering matches delta_algorithm_t (src/c/delta.h:85). */
+typedef enum {
+	DG_ALGO_GREEDY     = 0,
+	DG_ALGO_ONEPASS    = 1,
+	DG_ALGO_CORRECTING = 2
+} dg_algorithm_t;
+
+/* Option bits of delta_flags_t (src/c/delta.h:220-224). */
+#define DG_OPT_VERBOSE 0
+#define DG_OPT_SPLAY   1
+#define DG_OPT_INPLACE 2
+
+/* Layout- and meaning-identical to delta_diff_options_t (src/c/delta.h:248-257):
+ * p = seed length, q = hash table size floor (--table-size), buf_cap =
+ * correcting lookback capacity, max_table = correcting table ceiling. */
+typedef struct {
+	size_t   p;
+	size_t   q;
+	size_t   buf_cap;
+	size_t   max_table;
+	uint64_t flags;
+} dg_diff_options_t;
+
+/* DELTA_DIFF_OPTIONS_DEFAULT (src/c/delta.h:256-257). */
+void dg_diff_options_default(dg_diff_options_t *opts);
+
+/* A delta / output buffer; layout-identical to delta_buffer_t
+ * (src/c/delta.h:331-334).  Free with dg_buffer_free. */
+typedef struct {
+	uint8_t *data;
+	size_t   len;
+} dg_buffer_t;
+
+void dg_buffer_free(dg_buffer_t *buf);
+
+/* ── context ───────────────────────────────────────────────────────────── */
+
+typedef struct dg_context dg_context_t;
+
+/* Binds a HIP device (device < 0: the current device) and creates one HIP
+ * stream plus the constant tables.  Fails with DG_ERR_NO_DEVICE when no GPU
+ * is visible: there is no CPU fallback. */
+int  dg_context_create(int device, dg_context_t **out);
+void dg_context_destroy(dg_context_t *ctx);
+/* Current hipStream_t of the context, as void*. */
+void *dg_context_stream(dg_context_t *ctx);
+const char *dg_status_string(int status);
+/* Last error text recorded on this context (never NULL). */
+const char *dg_last_error(const dg_context_t *ctx);
+int dg_abi_version(void);
+
+/* ── batched, device-resident encode: the hot path ───────────────────────
+ *
+ * A batch is N independent (reference, version) pairs laid out in two device
+ * arenas.  A plan fixes the pair geometry and options once (table sizes,
+ * worst-case command capacity, work buffers, CRC segmentation) so that
+ * dg_encode_plan_run is pure device work on one stream (graph-capturable:
+ * no allocation, no host synchronisation).
+ *
+ * Output: one packed arena.  Pair i's delta occupies
+ * d_out[d_offsets[i] .. d_offsets[i+1]) and is byte-identical to the
+ * reference's `delta encode <algo> R_i V_i` output.  d_status[i] is a
+ * dg_status_t.  d_offsets has N+1 entries (d_offsets[N] = total bytes).
+ */
+typedef struct {
+	uint64_t r_off;   /* byte offset of R_i in the reference arena */
+	uint64_t r_len;
+	uint64_t v_off;   /* byte offset of V_i in the version arena */
+	uint64_t v_len;
+} dg_pair_t;
+
+typedef struct dg_encode_plan dg_encode_plan_t;
+
+int dg_encode_plan_create(dg_context_t *ctx, dg_algorithm_t algo,
+                          const dg_pair_t *pairs /* host */, uint32_t n_pairs,
+                          const dg_diff_options_t *opts,
+                          dg_encode_plan_t **out);
+/* Upper bound of the packed output (bytes): size d_out at least this. */
+uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t *plan);
+uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t *plan);
+/* Table size q actually used for pair i (onepass.c:61-62 /
+ * correcting.c:116-123 sizing). */
+uint64_t dg_encode_plan_table_size(const dg_encode_plan_t *plan, uint32_t i);
+int dg_encode_plan_run(dg_encode_plan_t *plan,
+                       const uint8_t *d_ref_arena, const uint8_t *d_ver_arena,
+                       uint8_t *d_out, uint64_t out_cap,
+                       uint64_t *d_offsets, int32_t *d_status,
+                       void *stream);
+/* Optional per-stage timing with HIP events on the run stream.  When enabled
+ * each run records events around every kernel; dg_encode_plan_stage_times
+ * fills up to `n` stage durations (ms) of the last run and their names.
+ * Returns the number of stages. */
+int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int enable);
+int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
+                               const char **names, int n);
+/* Per-pair command statistics of the last run (device pointers owned by the
+ * plan, valid until the next run): number of COPY commands and delta size. */
+const uint32_t *dg_encode_plan_copy_counts_device(const dg_encode_plan_t *plan);
+void dg_encode_plan_destroy(dg_encode_plan_t *plan);
+
+/* ── host-buffer convenience (end-to-end; includes PCIe transfers) ──────── */
+
+/* One pair: the chain of src/c/main.c:257-292, R and V in host memory.
+ * out->data is malloc'd; free with dg_buffer_free. */
+int dg_encode(dg_context_t *ctx, dg_algorithm_t algo,
+              const uint8_t *r, size_t r_len,
+              const uint8_t *v, size_t v_len,
+              const dg_diff_options_t *opts, dg_buffer_t *out);
+
+/* N pairs in host memory: pinned staging -> device -> host. outs[i] is
+ * malloc'd per pair; status[i] per pair (may be NULL). */
+int dg_encode_batch(dg_context_t *ctx, dg_algorithm_t algo,
+                    const uint8_t *const *r, const size_t *r_len,
+                    const uint8_t *const *v, const size_t *v_len,
+                    uint32_t n_pairs, const dg_diff_options_t *opts,
+                    dg_buffer_t *outs, int32_t *status);
+
+/* ── CRC-64/XZ (delta.h:294-322), computed on the device ──────────────── */
+
+typedef struct {
+	uint64_t off;   /* byte offset into the arena */
+	uint64_t len;
+} dg_span_t;
+
+/* CRC of a host buffer (copied to the device).  out = 8 bytes big-endian. */
+int dg_crc64_xz(dg_context_t *ctx, const uint8_t *data, size_t len,
+                uint8_t out[DG_CRC_SIZE]);
+/* CRC of N spans of one device arena; d_crc receives N u64 values (the CRC
+ * register value, not byte-swapped). spans are host descriptors. */
+int dg_crc64_xz_batch_device(dg_context_t *ctx, const uint8_t *d_arena,
+                             const dg_span_t *spans, uint32_t n,
+                             uint64_t *d_crc, void *stream);
+
+/* ── decode + apply + CRC verify (encoding.c:111-178, apply.c:229-284,
+ *    main.c:341-385) ────────────────────────────────────────────────────── */
+
+/* Decode one delta against R (host buffers).  Returns DG_OK,
+ * DG_ERR_MALFORMED, DG_ERR_SRC_CRC or DG_ERR_DST_CRC (the reference's exit
+ * paths); ignore_hash skips both CRC checks (main.c:330-333). */
+int dg_decode(dg_context_t *ctx, const uint8_t *r, size_t r_len,
+              const uint8_t *delta, size_t delta_len, int ignore_hash,
+              dg_buffer_t *out);
+
+/* Batched device decode: stream i is d_delta[delta_off[i] .. +delta_len[i])
+ * applied to d_ref[ref spans i]; output written to d_out at out_off[i]
+ * (capacity out_cap[i] >= version_size, and >= |R| for in-place deltas).
+ * d_status[i] receives a dg_status_t. Descriptors are host arrays. */
+typedef struct {
+	uint64_t ref_off, ref_len;
+	uint64_t delta_off, delta_len;
+	uint64_t out_off, out_cap;
+} dg_decode_desc_t;
+
+int dg_decode_batch_device(dg_context_t *ctx, const uint8_t *d_ref,
+                           const uint8_t *d_delta,
+                           const dg_decode_desc_t *descs, uint32_t n,
+                           int ignore_hash, uint8_t *d_out,
+                           uint64_t *d_out_len, int32_t *d_status,
+                           void *stream);
+
+/* ── delta inspection (host parse, src/c/main.c:402-425) ─────────────── */
+
+typedef struct {
+	int      inplace;
+	uint64_t version_size;
+	uint8_t  src_crc[DG_CRC_SIZE];
+	uint8_t  dst_crc[DG_CRC_SIZE];
+	uint64_t num_commands, num_copies, num_adds;
+	uint64_t copy_bytes, add_bytes;
+} dg_delta_info_t;
+
+int dg_delta_info(const uint8_t *delta, size_t len, dg_delta_info_t *info);
+
+/* ── synthetic batch generators (bench / test inputs, on the device) ─────
+ * Workload definitions in DESIGN.md ("Synthetic inputs"); the oracle's
+ * or_synth_* functions produce the same bytes on the CPU. */
+int dg_synth_edit_pairs_device(dg_context_t *ctx, uint8_t *d_ref,
+                               uint8_t *d_ver, uint32_t n_pairs,
+                               uint64_t pair_len, uint64_t seed_base,
+                               uint64_t n_edits, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DELTA_GPU_H */

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/golden.json from the REFERENCE itself.
+
+The reference's tests hold no golden delta bytes (encoder
+output is pinned only by cross-implementation byte identity), so the fixtures
+are minted here by running the reference's own src/c, compiled from
+/root/reference/src/c by oracle/Makefile (oracle/_ref/libdelta_ref.so,
+`ref_encode_pair` = the main.c:257-292 chain).  Run in the dev container:
+
+    make -C oracle ref && python tests/golden/make_golden.py
+
+Stored per case: inputs as sha256 (+ the generator spec, see tests/cases.py
+and DESIGN.md "Synthetic inputs"), the delta bytes (hex) when short, else
+sha256 + length, and the two CRCs.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import oracle as O  # noqa: E402
+from cases import small_cases  # noqa: E402
+
+INLINE_MAX = 2048
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def entry(ref, algo, R, V, p, q, **extra):
+    d = ref.encode(algo, R, V, p=p, q=q)
+    e = {"algo": algo, "p": p, "q": q, "r_sha256": sha(R), "v_sha256": sha(V),
+         "r_len": len(R), "v_len": len(V), "delta_len": len(d), "delta_sha256": sha(d),
+         "src_crc": d[9:17].hex(), "dst_crc": d[17:25].hex()}
+    if len(d) <= INLINE_MAX:
+        e["delta_hex"] = d.hex()
+    e.update(extra)
+    return e
+
+
+def main():
+    ref = O.Reference()
+    orc = O.Oracle()
+    out = {"generator": "reference src/c via oracle/_ref (ref_encode_pair)",
+           "crc_kat": {"123456789": "995dc9bbdf1939fa", "": "0000000000000000"},
+           "cases": []}
+    for name, R, V, p, q in small_cases():
+        for algo in (O.ONEPASS, O.CORRECTING):
+            if algo == O.CORRECTING and len(V) >= p and len(V) // 2 + p > len(V):
+                continue  # reference reads past |V| here (correcting.c:133-136): undefined
+            out["cases"].append(dict(name=name, kind="small", **entry(ref, algo, R, V, p, q)))
+    # synthetic workloads: first pairs of each config (DESIGN.md "Synthetic inputs")
+    synth = [
+        ("c2", 0xC2000000, 65536, 655, 1, 8),
+        ("c2_default_q", 0xC2000000, 65536, 655, 1048573, 2),
+        ("c3", 0xC3000000, 262144, 26214, 1, 4),
+    ]
+    for tag, seed, L, ne, q, count in synth:
+        for i in range(count):
+            R, V = orc.synth_pair(seed + i, L, ne)
+            out["cases"].append(dict(name=f"{tag}_{i}", kind="synth_edits", seed=seed + i,
+                                     pair_len=L, n_edits=ne, **entry(ref, O.ONEPASS, R, V, 16, q)))
+    for i in range(4):
+        nb = 8 + (i % 57)
+        R, V = orc.synth_transpose(0xC4000000 + i, nb, 262144 // nb, 50)
+        out["cases"].append(dict(name=f"c4_{i}", kind="synth_transpose", seed=0xC4000000 + i,
+                                 num_blocks=nb, mean=262144 // nb, pct=50,
+                                 **entry(ref, O.CORRECTING, R, V, 16, 1)))
+        out["cases"].append(dict(name=f"c4_onepass_{i}", kind="synth_transpose", seed=0xC4000000 + i,
+                                 num_blocks=nb, mean=262144 // nb, pct=50,
+                                 **entry(ref, O.ONEPASS, R, V, 16, 1)))
+    R = orc.synth_random(1, 1 << 20)
+    V = orc.synth_random(2, 1 << 20)
+    out["cases"].append(dict(name="c1_random_1MiB", kind="synth_random", r_seed=1, v_seed=2,
+                             **entry(ref, O.ONEPASS, R, V, 16, 1048573)))
+    path = os.path.join(HERE, "golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"wrote {len(out['cases'])} cases to {path}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,235 @@
+"""GPU parity: the HIP path against the oracle, bit for bit.
+
+Every comparison here is exact (integer/byte work).  The oracle is the CPU
+restatement in oracle/ (itself pinned to the reference in tests/test_oracle.py
+and tests/golden/).
+"""
+from __future__ import annotations
+
+import os
+import random
+
+import pytest
+
+from cases import DEFAULT_Q, random_cases, small_cases
+
+pytestmark = pytest.mark.gpu
+
+ONEPASS, CORRECTING = 1, 2
+
+
+# ── CRC-64/XZ ────────────────────────────────────────────────────────────
+
+def test_crc_known_answers(dg, ctx):
+    # src/python/test_delta.py:970-977, src/cpp/tests/test_hash.cpp:124-136
+    assert dg.crc64_xz(b"123456789", ctx=ctx).hex() == "995dc9bbdf1939fa"
+    assert dg.crc64_xz(b"", ctx=ctx) == bytes(8)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 15, 16, 17, 1000, 65535, 65536, 65537, 200001, 1 << 20])
+def test_crc_lengths(dg, ctx, orc, n):
+    data = random.Random(n).randbytes(n)
+    assert dg.crc64_xz(data, ctx=ctx) == orc.crc64_xz(data)
+
+
+def test_crc_batch_alignments(dg, ctx, orc, torch_cuda):
+    torch = torch_cuda
+    rng = random.Random(5)
+    blob = rng.randbytes(300000)
+    spans, exp = [], []
+    for i in range(200):
+        off = rng.randrange(0, 200000)
+        ln = rng.choice([0, 3, 8, 31, 64, 1000, 4097, 65536 + rng.randrange(64), 90000])
+        spans.append((off, ln))
+        exp.append(int.from_bytes(orc.crc64_xz(blob[off:off + ln]), "big"))
+    d = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    out = torch.zeros(len(spans), dtype=torch.int64, device="cuda")
+    import ctypes as C
+    arr = (dg._lib.Span * len(spans))(*[dg._lib.Span(o, l) for o, l in spans])
+    torch.cuda.synchronize()
+    ctx.check(dg.lib.dg_crc64_xz_batch_device(ctx.handle, d.data_ptr(), arr, len(spans),
+                                              out.data_ptr(), None), "crc batch")
+    got = [v & (2**64 - 1) for v in out.cpu().tolist()]
+    assert got == exp
+
+
+# ── onepass encode ───────────────────────────────────────────────────────
+
+@pytest.mark.parametrize("case", small_cases(), ids=lambda c: c[0])
+def test_onepass_small_cases(dg, ctx, orc, case):
+    name, R, V, p, q = case
+    got = dg.encode(R, V, "onepass", p=p, q=q, ctx=ctx)
+    assert got == orc.encode(ONEPASS, R, V, p=p, q=q)
+
+
+def test_onepass_random_batch(dg, ctx, orc):
+    cs = random_cases(300, seed=99)
+    by_pq = {}
+    for name, R, V, p, q in cs:
+        by_pq.setdefault((p, q), []).append((name, R, V))
+    for (p, q), items in by_pq.items():
+        got = dg.encode_batch([(R, V) for _, R, V in items], "onepass", p=p, q=q, ctx=ctx)
+        for (name, R, V), g in zip(items, got):
+            assert g == orc.encode(ONEPASS, R, V, p=p, q=q), name
+
+
+def _device_batch(dg, ctx, torch, n, L, rate, seed, algo="onepass", q=1, check=64):
+    ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    n_edits = int(rate * L + 0.5)
+    ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L,
+                                                seed, n_edits, None), "synth")
+    plan = dg.EncodePlan(ctx, algo, [(i * L, L, i * L, L) for i in range(n)], q=q)
+    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), off.data_ptr(),
+             st.data_ptr(), ctx.stream)
+    torch.cuda.synchronize()
+    return plan, ref, ver, out, off, st, n_edits
+
+
+def test_onepass_c2_batch_sample(dg, ctx, orc, torch_cuda):
+    """C2 geometry (64 KiB pairs, 1% edits, --table-size 1): device-generated
+    inputs equal the oracle's generator; sampled pairs bit-exact."""
+    torch = torch_cuda
+    n, L, seed = 256, 65536, 0xC2000000
+    plan, ref, ver, out, off, st, ne = _device_batch(dg, ctx, torch, n, L, 0.01, seed)
+    stc = st.cpu()
+    assert int(stc.abs().sum()) == 0
+    offs = off.cpu().tolist()
+    outc = out.cpu()
+    refc, verc = ref.cpu(), ver.cpu()
+    for i in list(range(0, n, 17)) + [n - 1]:
+        R, V = orc.synth_pair(seed + i, L, ne)
+        assert bytes(refc[i * L:(i + 1) * L].numpy()) == R
+        assert bytes(verc[i * L:(i + 1) * L].numpy()) == V
+        got = bytes(outc[offs[i]:offs[i + 1]].numpy())
+        assert got == orc.encode(ONEPASS, R, V, p=16, q=1), i
+
+
+# ── decode ───────────────────────────────────────────────────────────────
+
+@pytest.mark.parametrize("case", small_cases()[:24], ids=lambda c: c[0])
+def test_decode_roundtrip(dg, ctx, orc, case):
+    name, R, V, p, q = case
+    delta = orc.encode(ONEPASS, R, V, p=p, q=q)
+    assert dg.decode(R, delta, ctx=ctx) == V
+
+
+def test_decode_crc_errors(dg, ctx, orc):
+    R = random.Random(1).randbytes(3000)
+    V = R[:1000] + b"xyz" + R[1000:]
+    delta = orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q)
+    with pytest.raises(dg.DeltaError) as e:
+        dg.decode(R[:-1] + b"\x00", delta, ctx=ctx)
+    assert e.value.code == 9
+    bad = bytearray(delta)
+    bad[17] ^= 1
+    with pytest.raises(dg.DeltaError) as e:
+        dg.decode(R, bytes(bad), ctx=ctx)
+    assert e.value.code == 10
+    assert dg.decode(R, bytes(bad), ignore_hash=True, ctx=ctx) == V
+    with pytest.raises(dg.DeltaError) as e:
+        dg.decode(R, b"XLT\x03" + delta[4:], ctx=ctx)
+    assert e.value.code == 8
+
+
+# ── golden fixtures (minted from the reference) on the device ─────────────
+
+def _golden():
+    import json
+    here = os.path.dirname(os.path.abspath(__file__))
+    return json.load(open(os.path.join(here, "golden", "golden.json")))["cases"]
+
+
+def _golden_inputs(orc, case):
+    kind = case["kind"]
+    if kind == "small":
+        m = {c[0]: c for c in small_cases()}
+        return m[case["name"]][1], m[case["name"]][2]
+    if kind == "synth_edits":
+        return orc.synth_pair(case["seed"], case["pair_len"], case["n_edits"])
+    if kind == "synth_transpose":
+        return orc.synth_transpose(case["seed"], case["num_blocks"], case["mean"], case["pct"])
+    return orc.synth_random(case["r_seed"], 1 << 20), orc.synth_random(case["v_seed"], 1 << 20)
+
+
+def test_golden_onepass_on_device(dg, ctx, orc):
+    import hashlib
+    groups = {}
+    for c in _golden():
+        if c["algo"] != ONEPASS:
+            continue
+        groups.setdefault((c["p"], c["q"]), []).append(c)
+    for (p, q), cs in groups.items():
+        ins = [_golden_inputs(orc, c) for c in cs]
+        outs = dg.encode_batch(ins, "onepass", p=p, q=q, ctx=ctx)
+        for c, d in zip(cs, outs):
+            assert len(d) == c["delta_len"], c["name"]
+            assert hashlib.sha256(d).hexdigest() == c["delta_sha256"], c["name"]
+
+
+# ── full C2 batch: every pair decodes back to V on the device ─────────────
+
+def test_c2_full_batch_roundtrip(dg, ctx, orc, torch_cuda):
+    torch = torch_cuda
+    n, L, seed = 4096, 65536, 0xC2000000
+    plan, ref, ver, out, off, st, ne = _device_batch(dg, ctx, torch, n, L, 0.01, seed)
+    assert int(st.abs().sum()) == 0
+    offs = off.cpu()
+    import ctypes as C
+    descs = (dg._lib.DecodeDesc * n)(*[
+        dg._lib.DecodeDesc(i * L, L, int(offs[i]), int(offs[i + 1] - offs[i]), i * L, L)
+        for i in range(n)])
+    dec = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.check(dg.lib.dg_decode_batch_device(ctx.handle, ref.data_ptr(), out.data_ptr(), descs, n, 0,
+                                            dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(), None),
+              "decode batch")
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0          # src and dst CRC verified on device
+    assert bool(torch.equal(dec, ver))        # every V reproduced
+    # the first pairs equal the reference-minted golden deltas
+    import hashlib
+    gold = {c["name"]: c for c in _golden()}
+    outc = out.cpu()
+    for i in range(8):
+        d = bytes(outc[int(offs[i]):int(offs[i + 1])].numpy())
+        assert hashlib.sha256(d).hexdigest() == gold[f"c2_{i}"]["delta_sha256"]
+
+
+# ── CLI: same bytes and report lines as the reference CLI ─────────────────
+
+def test_cli_encode_decode_vs_reference(tmp_path, orc):
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    cli = os.path.join(os.path.dirname(here), "delta-compression_amd", "bin", "delta")
+    ref_cli = os.path.join(os.path.dirname(here), "oracle", "_ref", "delta")
+    R = orc.synth_random(1, 1 << 20)
+    V = orc.synth_random(2, 1 << 20)
+    rp, vp = tmp_path / "r.bin", tmp_path / "v.bin"
+    rp.write_bytes(R)
+    vp.write_bytes(V)
+    a = subprocess.run([cli, "encode", "onepass", str(rp), str(vp), str(tmp_path / "d")],
+                       capture_output=True, text=True)
+    assert a.returncode == 0, a.stderr
+    d = (tmp_path / "d").read_bytes()
+    assert len(d) == 1048611                  # C1: one ADD
+    assert d == orc.encode(ONEPASS, R, V)
+    if os.path.exists(ref_cli):
+        b = subprocess.run([ref_cli, "encode", "onepass", str(rp), str(vp), str(tmp_path / "d_ref")],
+                           capture_output=True, text=True)
+        assert (tmp_path / "d_ref").read_bytes() == d
+        strip = lambda s: [l for l in s.splitlines() if not l.startswith(("Time:", "Delta:"))]
+        assert strip(a.stdout) == strip(b.stdout)
+    c = subprocess.run([cli, "decode", str(rp), str(tmp_path / "d"), str(tmp_path / "out")],
+                       capture_output=True, text=True)
+    assert c.returncode == 0, c.stderr
+    assert (tmp_path / "out").read_bytes() == V
+    bad = subprocess.run([cli, "decode", str(vp), str(tmp_path / "d"), str(tmp_path / "out2")],
+                         capture_output=True, text=True)
+    assert bad.returncode == 1 and "source file does not match delta" in bad.stderr
