@@ -14,340 +14,9 @@
 #include <stdint.h>
 
 #include "dg_device.h"
+#include "dg_devutil.h"
 
 namespace dg {
-
-// ───────────────────────────── common helpers ─────────────────────────────
-
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
-
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
-	return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-__device__ __forceinline__ uint64_t mask_le(uint32_t j) {   // lanes 0..j
-	return j >= 63 ? ~0ULL : ((2ULL << j) - 1ULL);
-}
-
-__device__ __forceinline__ uint32_t ffs64(uint64_t m) {     // m != 0
-	return (uint32_t)__builtin_ctzll(m);
-}
-
-// x mod (2^61-1) for x < 2^63, canonical (src/c/hash.c:15-24).
-__device__ __forceinline__ uint64_t mod_m61(uint64_t x) {
-	uint64_t r = (x & kMersenne) + (x >> 61);
-	return r >= kMersenne ? r - kMersenne : r;
-}
-
-// x mod q by Barrett with magic = floor((2^64-1)/q).
-__device__ __forceinline__ uint64_t mod_q(uint64_t x, uint64_t q, uint64_t magic) {
-	uint64_t qh = __umul64hi(x, magic);
-	uint64_t r = x - qh * q;
-	if (r >= q) r -= q;
-	if (r >= q) r -= q;
-	return r;
-}
-
-// Karp-Rabin fingerprint of d[0..p) (src/c/hash.c:28-38) as a dot product
-// with the constants powc[k] = 263^(p-1-k) mod M: each term is an 8-bit x
-// 61-bit product, split into 32-bit halves so that both partial sums fit in
-// 64 bits; one fold at the end.
-template <int PF>
-__device__ __forceinline__ uint64_t window_fp(const uint8_t* d, uint32_t p,
-                                              const uint64_t* __restrict__ powc) {
-	uint64_t lo = 0, hi = 0;
-	if constexpr (PF > 0) {
-#pragma unroll
-		for (int k = 0; k < PF; ++k) {
-			const uint64_t c = powc[k];
-			const uint64_t b = d[k];
-			lo += b * (uint32_t)c;
-			hi += b * (uint32_t)(c >> 32);
-		}
-	} else {
-		for (uint32_t k = 0; k < p; ++k) {
-			const uint64_t c = powc[k];
-			const uint64_t b = d[k];
-			lo += b * (uint32_t)c;
-			hi += b * (uint32_t)(c >> 32);
-		}
-	}
-	// hi * 2^32 == (hi >> 29) * 2^61 + (hi & (2^29-1)) * 2^32 == (hi >> 29) + ...
-	const uint64_t t = lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29);
-	return mod_m61(t);
-}
-
-// Wave-parallel forward match extension (src/c/onepass.c:229-234): number of
-// equal leading bytes of a[] and b[], at most `limit`.  Uniform call.
-__device__ __noinline__ uint64_t extend_fwd(const uint8_t* a, const uint8_t* b,
-                                            uint64_t limit) {
-	const uint32_t lane = lane_id();
-	uint64_t ml = 0;
-	while (ml < limit) {
-		const uint64_t base = ml + 4ull * lane;
-		uint32_t bad = 4;
-#pragma unroll
-		for (int k = 3; k >= 0; --k) {
-			const uint64_t pos = base + k;
-			bool ok = false;
-			if (pos < limit) ok = a[pos] == b[pos];
-			if (!ok) bad = k;
-		}
-		const uint64_t m = __ballot(bad < 4);
-		if (m) {
-			const uint32_t f = ffs64(m);
-			return ml + 4ull * f + rdlane(bad, f);
-		}
-		ml += 256;
-	}
-	return limit;
-}
-
-// ───────────────────────────── onepass ────────────────────────────────────
-//
-// State between epochs is (v0, r0) only: every match bumps the table version
-// (onepass.c:263), so both tables are logically empty at an epoch start.
-// Step t of an epoch looks at V[v0+t..+p) and R[r0+t..+p).  Per step the
-// reference stores into HV/HR keeping the first writer of the version
-// (:141-166), then looks R's fingerprint up in HV, then V's in HR (:169-219).
-// So the candidate for lookup 1 at step t is the EARLIEST s <= t whose V-slot
-// equals R's slot at t; the match needs the bytes to agree (memcmp, :186);
-// equal bytes imply equal fingerprints, so the fingerprint test is only a
-// filter.
-//
-// Per epoch the wave evaluates 64 consecutive steps at once (lane = step):
-// fingerprints and slots in parallel, then walks the steps in order with
-// ballots over the slot history (register tier, up to kHistChunks chunks),
-// stopping at the first verified match.  Longer epochs move the history into
-// a per-pair (tag, step) table in HBM (table tier).
-
-struct TablePool {
-	unsigned long long* base;
-	uint64_t qmax;
-	uint32_t n;
-	uint32_t* locks;
-	uint32_t* tags;
-};
-
-__device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
-	return ((unsigned long long)tag << 32) | (0xFFFFFFFFu - rel);
-}
-
-__device__ __forceinline__ void tab_insert(unsigned long long* t, uint32_t slot,
-                                           uint32_t tag, uint32_t rel) {
-	if (slot != kSentinel)
-		__hip_atomic_fetch_max(t + slot, tab_key(tag, rel), __ATOMIC_RELAXED,
-		                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// earliest step stored in slot during this tag, or kSentinel
-__device__ __forceinline__ uint32_t tab_lookup(unsigned long long* t, uint32_t slot,
-                                               uint32_t tag, uint32_t max_rel) {
-	if (slot == kSentinel) return kSentinel;
-	// read at the memory side (an atomic no-op max): always coherent with the
-	// inserts above, whatever XCD last cached the line
-	unsigned long long e = __hip_atomic_fetch_max(t + slot, 0ull, __ATOMIC_RELAXED,
-	                                              __HIP_MEMORY_SCOPE_AGENT);
-	if ((uint32_t)(e >> 32) != tag) return kSentinel;
-	uint32_t rel = 0xFFFFFFFFu - (uint32_t)e;
-	return rel <= max_rel ? rel : kSentinel;
-}
-
-__device__ __forceinline__ void vm_drain() {
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int PF>
-__global__ __launch_bounds__(64) void onepass_kernel(EncodeArgs a) {
-	const uint32_t pair = blockIdx.x;
-	if (pair >= a.n_pairs) return;
-	const uint32_t lane = lane_id();
-	const PairDev pd = a.pairs[pair];
-	const PairPlanDev pp = a.pplan[pair];
-	const uint8_t* __restrict__ R = a.ref + pd.r_off;
-	const uint8_t* __restrict__ V = a.ver + pd.v_off;
-	const uint64_t rl = pd.r_len, vl = pd.v_len;
-	const uint32_t p = PF > 0 ? (uint32_t)PF : a.p;
-	const uint64_t q = pp.q, qmag = pp.q_magic;
-	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
-
-	uint32_t nrec = 0;
-	uint64_t dsz = 26;   // header (25) + END
-	int32_t st = 0;
-
-	// table tier state
-	int32_t tslot = -1;
-	uint32_t tag = 0;
-	unsigned long long* HV = nullptr;
-	unsigned long long* HR = nullptr;
-
-	uint64_t v0 = 0, r0 = 0;
-	bool scanning = vl > 0;
-	while (scanning) {
-		// early termination: no match is possible once either stream can no
-		// longer supply a window at the epoch start (onepass.c:102-104)
-		if (v0 + p > vl || r0 + p > rl) break;
-
-		uint32_t hsV[kHistChunks], hsR[kHistChunks], hfV[kHistChunks], hfR[kHistChunks];
-		bool matched = false;
-		bool in_table = false;
-		uint64_t vm = 0, rm = 0, ml = 0;
-
-		for (uint32_t c = 0; !matched; ++c) {
-			const uint64_t step = 64ull * c + lane;
-			const uint64_t vp = v0 + step, rp = r0 + step;
-			const bool cv = vp + p <= vl;
-			const bool cr = rp + p <= rl;
-			const uint64_t live = __ballot(cv || cr);
-			if (live == 0) { scanning = false; break; }   // both streams done
-			const uint32_t nlive = (uint32_t)__popcll(live);
-
-			uint64_t fV = 0, fR = 0;
-			uint32_t sV = kSentinel, sR = kSentinel;
-			if (cv) { fV = window_fp<PF>(V + vp, p, a.powc); sV = (uint32_t)mod_q(fV, q, qmag); }
-			if (cr) { fR = window_fp<PF>(R + rp, p, a.powc); sR = (uint32_t)mod_q(fR, q, qmag); }
-			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
-
-			if (c < (uint32_t)kHistChunks) {
-#pragma unroll
-				for (int k = 0; k < kHistChunks; ++k)
-					if ((uint32_t)k == c) { hsV[k] = sV; hsR[k] = sR; hfV[k] = fVl; hfR[k] = fRl; }
-
-				for (uint32_t j = 0; j < nlive && !matched; ++j) {
-					const uint64_t t = 64ull * c + j;
-					const bool ucr = r0 + t + p <= rl;
-					const bool ucv = v0 + t + p <= vl;
-					if (ucr) {
-						// lookup 1: R's slot at step t in the V history
-						const uint32_t x = rdlane(sR, j), xf = rdlane(fRl, j);
-						uint32_t s = kSentinel, sf = 0;
-#pragma unroll
-						for (int k = 0; k < kHistChunks; ++k) {
-							if (s == kSentinel && (uint32_t)k <= c) {
-								uint64_t m = __ballot(hsV[k] == x);
-								if ((uint32_t)k == c) m &= mask_le(j);
-								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfV[k], l); }
-							}
-						}
-						if (s != kSentinel && sf == xf) {
-							const uint64_t lim = min(vl - (v0 + s), rl - (r0 + t));
-							const uint64_t e = extend_fwd(V + v0 + s, R + r0 + t, lim);
-							if (e >= p) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; }
-						}
-					}
-					if (!matched && ucv) {
-						// lookup 2: V's slot at step t in the R history
-						const uint32_t x = rdlane(sV, j), xf = rdlane(fVl, j);
-						uint32_t s = kSentinel, sf = 0;
-#pragma unroll
-						for (int k = 0; k < kHistChunks; ++k) {
-							if (s == kSentinel && (uint32_t)k <= c) {
-								uint64_t m = __ballot(hsR[k] == x);
-								if ((uint32_t)k == c) m &= mask_le(j);
-								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfR[k], l); }
-							}
-						}
-						if (s != kSentinel && sf == xf) {
-							const uint64_t lim = min(vl - (v0 + t), rl - (r0 + s));
-							const uint64_t e = extend_fwd(V + v0 + t, R + r0 + s, lim);
-							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; }
-						}
-					}
-				}
-			} else {
-				// ── table tier: epoch longer than the register history ──
-				if (!in_table) {
-					in_table = true;
-					if (tslot < 0) {
-						// acquire a table from the pool (bounded spin)
-						uint32_t got = 0xFFFFFFFFu;
-						if (lane == 0) {
-							const uint32_t n = a.n_tables;
-							for (uint32_t it = 0; it < (1u << 26) && got == 0xFFFFFFFFu; ++it) {
-								const uint32_t sl = (pair + it) % n;
-								if (atomicCAS(&a.table_locks[sl], 0u, 1u) == 0u) got = sl;
-								else if ((it % n) == n - 1) __builtin_amdgcn_s_sleep(8);
-							}
-						}
-						got = rdlane(got, 0);
-						if (got == 0xFFFFFFFFu) { st = 5; scanning = false; break; }
-						tslot = (int32_t)got;
-						HV = a.tables + (uint64_t)got * 2ull * a.qmax;
-						HR = HV + a.qmax;
-						uint32_t t0 = 0;
-						if (lane == 0)
-							t0 = __hip_atomic_load(&a.table_tags[got], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-						tag = rdlane(t0, 0);
-					}
-					if (tag == 0xFFFFFFFFu) {   // tag space exhausted: clear
-						for (uint64_t i = lane; i < 2ull * a.qmax; i += 64)
-							__hip_atomic_store(HV + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-						vm_drain();
-						tag = 0;
-					}
-					++tag;
-#pragma unroll
-					for (int k = 0; k < kHistChunks; ++k) {
-						tab_insert(HV, hsV[k], tag, 64u * k + lane);
-						tab_insert(HR, hsR[k], tag, 64u * k + lane);
-					}
-				}
-				tab_insert(HV, sV, tag, (uint32_t)step);
-				tab_insert(HR, sR, tag, (uint32_t)step);
-				vm_drain();
-				const uint32_t c1 = cr ? tab_lookup(HV, sR, tag, (uint32_t)step) : kSentinel;
-				const uint32_t c2 = cv ? tab_lookup(HR, sV, tag, (uint32_t)step) : kSentinel;
-				const uint64_t any = __ballot(c1 != kSentinel || c2 != kSentinel);
-				if (any) {
-					for (uint32_t j = 0; j < nlive && !matched; ++j) {
-						if (!((any >> j) & 1)) continue;
-						const uint64_t t = 64ull * c + j;
-						const uint32_t s1 = rdlane(c1, j);
-						if (s1 != kSentinel) {
-							const uint64_t lim = min(vl - (v0 + s1), rl - (r0 + t));
-							const uint64_t e = extend_fwd(V + v0 + s1, R + r0 + t, lim);
-							if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; }
-						}
-						const uint32_t s2 = rdlane(c2, j);
-						if (!matched && s2 != kSentinel) {
-							const uint64_t lim = min(vl - (v0 + t), rl - (r0 + s2));
-							const uint64_t e = extend_fwd(V + v0 + t, R + r0 + s2, lim);
-							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; }
-						}
-					}
-				}
-			}
-		}
-		if (!matched) break;
-
-		// emit ADD (implicit gap) + COPY, then flush the tables (:243-263)
-		if (nrec >= pp.rec_cap) { st = 7; break; }
-		if (lane == 0) {
-			rec[3u * nrec + 0] = (uint32_t)vm;
-			rec[3u * nrec + 1] = (uint32_t)rm;
-			rec[3u * nrec + 2] = (uint32_t)ml;
-		}
-		++nrec;
-		dsz += 13 + (vm > v0 ? 9 + (vm - v0) : 0);
-		v0 = vm + ml;
-		r0 = rm + ml;
-	}
-	if (v0 < vl) dsz += 9 + (vl - v0);   // trailing ADD (:268-275)
-
-	if (tslot >= 0 && lane == 0) {
-		__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		vm_drain();
-		__hip_atomic_store(&a.table_locks[tslot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-	}
-	if (lane == 0) {
-		a.n_rec[pair] = nrec;
-		a.dsize[pair] = dsz;
-		a.status[pair] = st;
-	}
-}
-
-template __global__ void onepass_kernel<16>(EncodeArgs);
-template __global__ void onepass_kernel<0>(EncodeArgs);
 
 // ───────────────────────────── scan of sizes ──────────────────────────────
 
@@ -539,9 +208,11 @@ __device__ uint64_t gf2_mulmod(uint64_t a, uint64_t b) {
 
 // keep-mask of bytes [lo, hi) within an 8-byte word (0 <= lo, hi <= 8)
 __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
+	lo = lo < 0 ? 0 : lo;   // clamp first: a negative shift count is undefined
+	hi = hi > 8 ? 8 : hi;   // (gfx950 would use its low 6 bits)
 	if (hi <= lo) return 0;
-	const uint64_t up = hi >= 8 ? ~0ULL : ((1ULL << (8 * hi)) - 1);
-	const uint64_t dn = lo <= 0 ? 0ULL : ((1ULL << (8 * lo)) - 1);
+	const uint64_t up = hi == 8 ? ~0ULL : ((1ULL << (8 * hi)) - 1);
+	const uint64_t dn = lo == 0 ? 0ULL : ((1ULL << (8 * lo)) - 1);
 	return up & ~dn;
 }
 
@@ -665,15 +336,6 @@ __global__ __launch_bounds__(64) void synth_edits_kernel(uint8_t* ver, uint32_t 
 // ───────────────────────────── launchers (C++ linkage, internal) ──────────
 
 namespace dg {
-
-hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, hipStream_t st) {
-	if (a.n_pairs == 0) return hipSuccess;
-	if (p == 16)
-		hipLaunchKernelGGL(onepass_kernel<16>, dim3(a.n_pairs), dim3(64), 0, st, a);
-	else
-		hipLaunchKernelGGL(onepass_kernel<0>, dim3(a.n_pairs), dim3(64), 0, st, a);
-	return hipGetLastError();
-}
 
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
