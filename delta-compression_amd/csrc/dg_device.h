@@ -124,7 +124,7 @@ struct DecodeArgs {
 
 // launchers (dg_kernels.hip)
 #ifdef __HIP_PLATFORM_AMD__
-hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, hipStream_t st);
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);

@@ -291,6 +291,7 @@ struct dg_encode_plan {
 	uint64_t total_rec = 0;
 	uint64_t qmax = 0;
 	uint32_t n_tables = 0;
+	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
 	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_cand;
@@ -339,10 +340,13 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	const uint64_t p = o.p;
 	for (uint32_t i = 0; i < n; ++i) {
 		const dg_pair_t& d = pairs[i];
-		if (d.r_len >= (1ull << 32) || d.v_len >= (1ull << 32)) {
+		// the format's u32 fields cap every buffer below 4 GiB (encoding.c:63,72-78);
+		// the kernels keep 32-bit cursors with 1 MiB of headroom
+		if (d.r_len >= (1ull << 32) - (1ull << 20) || d.v_len >= (1ull << 32) - (1ull << 20)) {
 			delete P;
 			return set_err(ctx, DG_ERR_TOO_LARGE, "pair %u: buffers of 4 GiB or more do not fit the u32 format", i);
 		}
+		if ((d.r_off | d.v_off) & 15) P->aligned16 = false;
 		PairPlanDev& x = P->pp[i];
 		memset(&x, 0, sizeof x);
 		const uint64_t seeds = d.r_len >= p ? d.r_len - p + 1 : 0;
@@ -529,7 +533,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)std::min<size_t>(P->opts.buf_cap, 1u << 20);
 		if (P->algo == DG_ALGO_ONEPASS)
-			HIPCHK(ctx, launch_onepass(a, a.p, st));
+			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 		else
 			HIPCHK(ctx, launch_correcting(a, a.p, st));
 	}

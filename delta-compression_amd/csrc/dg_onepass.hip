@@ -18,7 +18,9 @@
 // Equal bytes imply equal fingerprints, so the stored fingerprint test of the
 // reference is only a filter here.  Slots are fp mod q exactly as in the
 // reference, so collisions — and therefore the output — depend on q the same
-// way.
+// way.  Steps where V (R) has no full window insert nothing
+// into HV (HR) and skip lookup 2 (1); the scan ends when neither stream has a
+// window left (:102-104).
 //
 // Evaluation per epoch:
 //   phase A (p = 16): steps 0..7 at once, 4 lanes per window (most epochs
@@ -29,12 +31,16 @@
 //                     (kHistChunks chunks);
 //   phase C:          epochs longer than the register history insert their
 //                     (slot -> earliest step) entries into a per-pair table in
-//                     HBM tagged with a per-epoch tag (no clearing).
-// Bytes come from per-wave LDS windows over V and R (p = 16): both cursors
-// only move forward within a pair, so a 4 KiB window per stream is refilled
-// with coalesced 16-byte loads every few dozen epochs instead of paying two
-// dependent HBM round trips per epoch.  Other seed lengths read HBM/L2
-// directly.
+//                     HBM under a per-epoch tag (never cleared).
+// Bytes come from per-wave LDS windows over V and R (p = 16, 16-byte aligned
+// pairs): both cursors only move forward within a pair, so a 4 KiB window per
+// stream is refilled by LDS-DMA every few dozen epochs instead of paying two
+// dependent HBM round trips per epoch.  Other seed lengths / unaligned pairs
+// read HBM/L2 directly.
+//
+// All cursors are 32-bit (the format caps buffers below 4 GiB) and every
+// per-epoch decision is made on wave-uniform values, so the scalar unit — not
+// exec-mask juggling — runs the control flow.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -43,6 +49,34 @@
 #include "dg_devutil.h"
 
 namespace dg {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// ───────────────────────────── small helpers ──────────────────────────────
+
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// x + (lane ^ 1) and x + (lane ^ 2) within quads, via DPP (no LDS traffic)
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ uint64_t quad_sum64(uint64_t x) {
+	uint64_t y = ((uint64_t)dpp_xor1((uint32_t)(x >> 32)) << 32) | dpp_xor1((uint32_t)x);
+	x += y;
+	y = ((uint64_t)dpp_xor2((uint32_t)(x >> 32)) << 32) | dpp_xor2((uint32_t)x);
+	return x + y;
+}
+
+__device__ __forceinline__ uint64_t fold61(uint64_t lo, uint64_t hi) {
+	// lo + hi * 2^32 mod (2^61 - 1), lo < 2^48, hi < 2^45
+	return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
+}
 
 // ───────────────────────────── table tier ─────────────────────────────────
 
@@ -72,7 +106,7 @@ __device__ __forceinline__ uint32_t tab_lookup(unsigned long long* t, uint32_t s
 
 // ───────────────────────────── byte sources ───────────────────────────────
 
-// Generic seed length: windows and extensions read HBM/L2 directly.
+// Any seed length / alignment: windows and extensions read HBM/L2 directly.
 template <int PF>
 struct GlobalSrc {
 	static constexpr bool kPhaseA = false;
@@ -80,77 +114,74 @@ struct GlobalSrc {
 	const uint8_t* R;
 	uint32_t p;
 	const uint64_t* powc;
-	__device__ void chunk(uint64_t, uint64_t, bool) {}
-	__device__ uint64_t fpV(uint64_t pos) { return window_fp<PF>(V + pos, p, powc); }
-	__device__ uint64_t fpR(uint64_t pos) { return window_fp<PF>(R + pos, p, powc); }
-	__device__ uint64_t extend(uint64_t vpos, uint64_t rpos, uint64_t lim) {
-		return uni64(extend_fwd(V + vpos, R + rpos, lim));
+	__device__ void chunk(uint32_t, uint32_t, bool, bool) {}
+	__device__ uint64_t fpV(uint32_t pos) { return window_fp<PF>(V + pos, p, powc); }
+	__device__ uint64_t fpR(uint32_t pos) { return window_fp<PF>(R + pos, p, powc); }
+	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
+		return uni((uint32_t)extend_fwd(V + vpos, R + rpos, lim));
 	}
 };
 
-typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr uint32_t kWin = 4096;             // bytes per stream window
+constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 
-constexpr int kWin = 4096;                 // bytes per stream window
-constexpr int kWinStride = kWin + 16;      // + slack for the 2nd dword of rd4
-
-// p = 16: sliding LDS windows over both streams.
+// p = 16 and 16-byte aligned stream bases: sliding LDS windows.
 struct WinSrc {
 	static constexpr bool kPhaseA = true;
-	const uint8_t* S[2];     // V, R
-	uint64_t len[2];
-	int64_t base[2];         // stream offset held at win[s][0] (wave-uniform)
-	uint8_t* win;            // LDS, 2 x kWinStride
+	const uint8_t* S[2];     // V, R (16-byte aligned)
+	uint32_t len[2];
+	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
+	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
 	const uint64_t* powc;
 
-	// (re)load whichever windows do not cover [lo, lo+need); both streams'
-	// loads are issued before either is waited for
-	__device__ void ensure2(int64_t vlo, int64_t rlo, int need, bool wantV, bool wantR) {
+	// (re)load whichever window does not cover [lo, lo+need); both streams'
+	// LDS-DMA requests are in flight before the single wait
+	__device__ void ensure2(uint32_t vlo, uint32_t rlo, uint32_t need, bool wantV, bool wantR) {
 		const bool fv = wantV && (vlo < base[0] || vlo + need > base[0] + kWin);
 		const bool fr = wantR && (rlo < base[1] || rlo + need > base[1] + kWin);
 		if (!fv && !fr) return;
 		const uint32_t lane = lane_id();
-		__syncthreads();   // the wave's reads of the old windows are complete
-		// LDS-DMA: lane l's 16 source bytes land at lds + 16*l (lane-linear),
-		// no VGPR staging.  The new base keeps every source block 16-byte
-		// aligned in memory, so a block holding any stream byte cannot cross
-		// a page; blocks wholly outside the stream are skipped (their window
-		// bytes are never consumed: every use is bounded by |V| or |R|).
+		__syncthreads();   // the wave's reads of the old window are complete
+		// lane l's 16 bytes land at lds + 16*l (lane-linear).  Blocks past the
+		// stream end are skipped: their window bytes are never consumed, every
+		// use being bounded by |V| or |R|; a block holding any stream byte is
+		// 16-byte aligned and cannot cross a page.
 		if (fv) {
-			const int64_t nb = vlo - (int64_t)(((uintptr_t)(S[0] + vlo)) & 15);
+			const uint32_t nb = vlo & ~15u;
 #pragma unroll
-			for (int k = 0; k < kWin / 1024; ++k) {
-				const int64_t off = nb + 1024 * k + 16 * lane;
-				if (off < (int64_t)len[0] && off + 16 > 0)
+			for (uint32_t k = 0; k < kWin / 1024; ++k) {
+				const uint32_t off = nb + 1024 * k + 16 * lane;
+				if (off < len[0])
 					__builtin_amdgcn_global_load_lds((const void*)(S[0] + off),
 					                                 (lds_void_t*)(win + 1024 * k), 16, 0, 0);
 			}
 			base[0] = nb;
 		}
 		if (fr) {
-			const int64_t nb = rlo - (int64_t)(((uintptr_t)(S[1] + rlo)) & 15);
+			const uint32_t nb = rlo & ~15u;
 #pragma unroll
-			for (int k = 0; k < kWin / 1024; ++k) {
-				const int64_t off = nb + 1024 * k + 16 * lane;
-				if (off < (int64_t)len[1] && off + 16 > 0)
+			for (uint32_t k = 0; k < kWin / 1024; ++k) {
+				const uint32_t off = nb + 1024 * k + 16 * lane;
+				if (off < len[1])
 					__builtin_amdgcn_global_load_lds((const void*)(S[1] + off),
 					                                 (lds_void_t*)(win + kWinStride + 1024 * k), 16, 0, 0);
 			}
 			base[1] = nb;
 		}
-		vm_drain();        // DMA landed (ordered by vmcnt) ...
+		vm_drain();        // the DMA landed (ordered by vmcnt) ...
 		__syncthreads();   // ... and is visible to every lane
 	}
 
 	// 4 bytes of stream s at offset x (little-endian), x inside the window
-	__device__ __forceinline__ uint32_t rd4(uint32_t s, int64_t x) const {
-		const uint32_t i = (uint32_t)(x - (s ? base[1] : base[0]));
-		const uint8_t* w = win + (s ? kWinStride : 0) + (i & ~3u);
-		const uint32_t w0 = *reinterpret_cast<const uint32_t*>(w);
-		const uint32_t w1 = *reinterpret_cast<const uint32_t*>(w + 4);
+	__device__ __forceinline__ uint32_t rd4(uint32_t s, uint32_t x) const {
+		const uint32_t i = x - (s ? base[1] : base[0]);
+		const lds_u32* w = (const lds_u32*)(win + (s ? kWinStride : 0) + (i & ~3u));
+		const uint32_t w0 = w[0];
+		const uint32_t w1 = w[1];
 		return __builtin_amdgcn_alignbyte(w1, w0, i & 3u);
 	}
 
-	__device__ __forceinline__ uint64_t fp16(uint32_t s, int64_t x) const {
+	__device__ __forceinline__ uint64_t fp16(uint32_t s, uint32_t x) const {
 		uint64_t lo = 0, hi = 0;
 #pragma unroll
 		for (int g = 0; g < 4; ++g) {
@@ -163,31 +194,30 @@ struct WinSrc {
 				hi += b * (uint32_t)(c >> 32);
 			}
 		}
-		return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
+		return fold61(lo, hi);
 	}
 
 	// windows for a 64-step chunk starting at (vpos, rpos)
-	__device__ void chunk(uint64_t vpos, uint64_t rpos, bool any) {
-		if (any) ensure2((int64_t)vpos, (int64_t)rpos, 64 + 16 + 8, vpos < len[0], rpos < len[1]);
+	__device__ void chunk(uint32_t vpos, uint32_t rpos, bool wantV, bool wantR) {
+		ensure2(vpos, rpos, 64 + 16 + 8, wantV, wantR);
 	}
-	__device__ uint64_t fpV(uint64_t pos) const { return fp16(0, (int64_t)pos); }
-	__device__ uint64_t fpR(uint64_t pos) const { return fp16(1, (int64_t)pos); }
+	__device__ uint64_t fpV(uint32_t pos) const { return fp16(0, pos); }
+	__device__ uint64_t fpR(uint32_t pos) const { return fp16(1, pos); }
 
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
-	__device__ uint64_t extend(uint64_t vpos, uint64_t rpos, uint64_t lim) {
+	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
 		const uint32_t lane = lane_id();
-		uint64_t ml = 0;
+		uint32_t ml = 0;
 		while (ml < lim) {
-			ensure2((int64_t)(vpos + ml), (int64_t)(rpos + ml), 256 + 8, true, true);
-			const uint32_t x = rd4(0, (int64_t)(vpos + ml + 4 * lane)) ^
-			                   rd4(1, (int64_t)(rpos + ml + 4 * lane));
+			ensure2(vpos + ml, rpos + ml, 256 + 8, true, true);
+			const uint32_t x = rd4(0, vpos + ml + 4 * lane) ^ rd4(1, rpos + ml + 4 * lane);
 			uint32_t fb = x ? ((uint32_t)__builtin_ctz(x) >> 3) : 4u;
-			const int64_t rem = (int64_t)lim - (int64_t)(ml + 4 * lane);
-			if (rem < (int64_t)fb) fb = rem < 0 ? 0u : (uint32_t)rem;
+			const int32_t rem = (int32_t)umin32(lim - ml, 512u) - (int32_t)(4 * lane);
+			if (rem < (int32_t)fb) fb = rem < 0 ? 0u : (uint32_t)rem;
 			const uint64_t m = __ballot(fb < 4);
 			if (m) {
 				const uint32_t f = ffs64(m);
-				return ml + 4ull * f + rdlane(fb, f);
+				return ml + 4 * f + rdlane(fb, f);
 			}
 			ml += 256;
 		}
@@ -195,43 +225,47 @@ struct WinSrc {
 	}
 };
 
-// ───────────────────────────── kernel ─────────────────────────────────────
+// ───────────────────────────── the epoch chain ────────────────────────────
 
 template <class Src>
 __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
-                                             const uint64_t (&cA)[4]) {
+                                             const uint64_t (&cA)[4], uint32_t* bm) {
 	const uint32_t lane = lane_id();
-	const uint64_t rl = pd.r_len, vl = pd.v_len;
-	const uint64_t q = pp.q, qmag = pp.q_magic;
+	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
+	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
+	const uint32_t rec_cap = uni(pp.rec_cap);
 	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
 
 	uint32_t nrec = 0;
 	uint64_t dsz = 26;   // header (25) + END
 	int32_t st = 0;
+	// COPY records staged in VGPRs (lane k holds record k mod 64)
+	uint32_t sv = 0, sr = 0, sl = 0;
 
 	int32_t tslot = -1;  // table tier state
 	uint32_t tag = 0;
 	unsigned long long* HV = nullptr;
 	unsigned long long* HR = nullptr;
 
-	uint64_t v0 = 0, r0 = 0;
+	uint32_t v0 = 0, r0 = 0;
 	bool scanning = vl > 0;
 	while (scanning) {
 		// no match is possible once either stream cannot supply a window at
-		// the epoch start (onepass.c:102-104 keeps scanning the other one)
+		// the epoch start (the reference keeps scanning the other, :102-104)
 		if (v0 + p > vl || r0 + p > rl) break;
+		const uint32_t nv = vl - p - v0 + 1;   // steps with a V window
+		const uint32_t nr = rl - p - r0 + 1;   // steps with an R window
+		const uint32_t nlive = umax32(nv, nr);
 
 		bool matched = false;
-		uint64_t vm = 0, rm = 0, ml = 0;
+		uint32_t vm = 0, rm = 0, ml = 0;
 
 		// ── phase A: steps 0..7, four lanes per window ──
 		if constexpr (Src::kPhaseA) {
-			src.ensure2((int64_t)v0, (int64_t)r0, 8 + 16 + 8, true, true);
+			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
 			const uint32_t side = lane >> 5, w = (lane >> 2) & 7u, part = lane & 3u;
-			const uint64_t spos = (side ? r0 : v0) + w;
-			const bool valid = spos + 16 <= (side ? rl : vl);
-			const uint32_t bytes = src.rd4(side, (int64_t)(spos + 4 * part));
+			const uint32_t bytes = src.rd4(side, (side ? r0 : v0) + w + 4 * part);
 			uint64_t lo = 0, hi = 0;
 #pragma unroll
 			for (int j = 0; j < 4; ++j) {
@@ -239,74 +273,84 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 				lo += b * (uint32_t)cA[j];
 				hi += b * (uint32_t)(cA[j] >> 32);
 			}
-			lo += __shfl_xor(lo, 1, 64);
-			hi += __shfl_xor(hi, 1, 64);
-			lo += __shfl_xor(lo, 2, 64);
-			hi += __shfl_xor(hi, 2, 64);
-			const uint64_t fp = mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
+			const uint64_t fp = fold61(quad_sum64(lo), quad_sum64(hi));
+			const bool valid = w < (side ? nr : nv);
 			const uint32_t slot = valid ? (uint32_t)mod_q(fp, q, qmag) : kSentinel;
 			const uint32_t fpl = (uint32_t)fp;
-			const bool head = part == 0;
-			for (uint32_t t = 0; t < 8 && !matched; ++t) {
-				const bool ucr = r0 + t + 16 <= rl, ucv = v0 + t + 16 <= vl;
-				if (!ucr && !ucv) { scanning = false; break; }
-				if (ucr) {
-					const uint32_t x = rdlane(slot, 32 + 4 * t), xf = rdlane(fpl, 32 + 4 * t);
-					const uint64_t m = __ballot(side == 0 && head && w <= t && slot == x);
+			const uint32_t tA = umin32(8u, nlive);
+			for (uint32_t t = 0; t < tA; ++t) {
+				if (t < nr) {   // lookup 1: R(t) in the V heads of steps 0..t
+					const uint32_t x = rdlane(slot, 32 + 4 * t);
+					const uint64_t m = __ballot(slot == x) & 0x11111111ull & ((2ull << (4 * t)) - 1);
 					if (m) {
-						const uint32_t l = ffs64(m), s = l >> 2;
-						if (rdlane(fpl, l) == xf) {
-							const uint64_t e = src.extend(v0 + s, r0 + t, min(vl - (v0 + s), rl - (r0 + t)));
-							if (e >= 16) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; }
+						const uint32_t l = ffs64(m);
+						if (rdlane(fpl, l) == rdlane(fpl, 32 + 4 * t)) {
+							const uint32_t s = l >> 2;
+							const uint32_t e = src.extend(v0 + s, r0 + t, umin32(vl - (v0 + s), rl - (r0 + t)));
+							if (e >= 16) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; break; }
 						}
 					}
 				}
-				if (!matched && ucv) {
-					const uint32_t x = rdlane(slot, 4 * t), xf = rdlane(fpl, 4 * t);
-					const uint64_t m = __ballot(side == 1 && head && w <= t && slot == x);
+				if (t < nv) {   // lookup 2: V(t) in the R heads of steps 0..t
+					const uint32_t x = rdlane(slot, 4 * t);
+					const uint64_t m = __ballot(slot == x) & 0x1111111100000000ull & ((2ull << (32 + 4 * t)) - 1);
 					if (m) {
-						const uint32_t l = ffs64(m), s = (l - 32) >> 2;
-						if (rdlane(fpl, l) == xf) {
-							const uint64_t e = src.extend(v0 + t, r0 + s, min(vl - (v0 + t), rl - (r0 + s)));
-							if (e >= 16) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; }
+						const uint32_t l = ffs64(m);
+						if (rdlane(fpl, l) == rdlane(fpl, 4 * t)) {
+							const uint32_t s = (l - 32) >> 2;
+							const uint32_t e = src.extend(v0 + t, r0 + s, umin32(vl - (v0 + t), rl - (r0 + s)));
+							if (e >= 16) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; break; }
 						}
 					}
 				}
 			}
-			if (!scanning) break;
+			if (!matched && nlive <= 8) break;   // both streams exhausted: scan over
 		}
 
 		// ── phases B and C: 64 steps per chunk ──
 		uint32_t hsV[kHistChunks], hsR[kHistChunks], hfV[kHistChunks], hfR[kHistChunks];
 		bool in_table = false;
 		for (uint32_t c = 0; !matched; ++c) {
-			const uint64_t step = 64ull * c + lane;
-			const uint64_t vp = v0 + step, rp = r0 + step;
-			const bool cv = vp + p <= vl;
-			const bool cr = rp + p <= rl;
-			const uint64_t live = __ballot(cv || cr);
-			if (live == 0) { scanning = false; break; }   // both streams exhausted
-			const uint32_t nlive = (uint32_t)__popcll(live);
-			src.chunk(v0 + 64ull * c, r0 + 64ull * c, true);
+			const uint32_t b0 = 64 * c;
+			if (b0 >= nlive) { scanning = false; break; }   // both streams exhausted
+			const uint32_t nl = umin32(64u, nlive - b0);
+			const uint32_t step = b0 + lane;
+			const bool cv = step < nv, cr = step < nr;
+			src.chunk(v0 + b0, r0 + b0, b0 < nv, b0 < nr);
 
 			uint64_t fV = 0, fR = 0;
 			uint32_t sV = kSentinel, sR = kSentinel;
-			if (cv) { fV = src.fpV(vp); sV = (uint32_t)mod_q(fV, q, qmag); }
-			if (cr) { fR = src.fpR(rp); sR = (uint32_t)mod_q(fR, q, qmag); }
+			if (cv) { fV = src.fpV(v0 + step); sV = (uint32_t)mod_q(fV, q, qmag); }
+			if (cr) { fR = src.fpR(r0 + step); sR = (uint32_t)mod_q(fR, q, qmag); }
 			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
 
 			if (c < (uint32_t)kHistChunks) {
 #pragma unroll
 				for (int k = 0; k < kHistChunks; ++k)
 					if ((uint32_t)k == c) { hsV[k] = sV; hsR[k] = sR; hfV[k] = fVl; hfR[k] = fRl; }
-				// steps a phase-A pass already ruled out are skipped
+				// Filter: a 2048-bit hash of every slot inserted in this epoch
+				// so far, per table.  A step whose slot misses the other
+				// table's bitmap has no candidate at all; only the remaining
+				// steps are walked exactly (in step order).
+				if (c == 0) { bm[lane] = 0u; bm[64 + lane] = 0u; }
+				__builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+				__builtin_amdgcn_wave_barrier();
+				if (cv) atomicOr(&bm[(sV >> 5) & 63u], 1u << (sV & 31u));
+				if (cr) atomicOr(&bm[64 + ((sR >> 5) & 63u)], 1u << (sR & 31u));
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+				const bool p1 = cr && ((bm[(sR >> 5) & 63u] >> (sR & 31u)) & 1u);
+				const bool p2 = cv && ((bm[64 + ((sV >> 5) & 63u)] >> (sV & 31u)) & 1u);
+				const uint64_t m1 = __ballot(p1), m2 = __ballot(p2);
+				// steps phase A already ruled out are skipped
 				const uint32_t j0 = (Src::kPhaseA && c == 0) ? 8u : 0u;
-				for (uint32_t j = j0; j < nlive && !matched; ++j) {
-					const uint64_t t = 64ull * c + j;
-					const bool ucr = r0 + t + p <= rl;
-					const bool ucv = v0 + t + p <= vl;
-					if (ucr) {
-						const uint32_t x = rdlane(sR, j), xf = rdlane(fRl, j);
+				uint64_t walk = (m1 | m2) & ~((1ull << j0) - 1ull);
+				while (walk) {
+					const uint32_t j = ffs64(walk);
+					walk &= walk - 1;
+					const uint32_t t = b0 + j;
+					if ((m1 >> j) & 1u) {
+						const uint32_t x = rdlane(sR, j);
 						uint32_t s = kSentinel, sf = 0;
 #pragma unroll
 						for (int k = 0; k < kHistChunks; ++k) {
@@ -316,13 +360,13 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfV[k], l); }
 							}
 						}
-						if (s != kSentinel && sf == xf) {
-							const uint64_t e = src.extend(v0 + s, r0 + t, min(vl - (v0 + s), rl - (r0 + t)));
-							if (e >= p) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; }
+						if (s != kSentinel && sf == rdlane(fRl, j)) {
+							const uint32_t e = src.extend(v0 + s, r0 + t, umin32(vl - (v0 + s), rl - (r0 + t)));
+							if (e >= p) { matched = true; vm = v0 + s; rm = r0 + t; ml = e; break; }
 						}
 					}
-					if (!matched && ucv) {
-						const uint32_t x = rdlane(sV, j), xf = rdlane(fVl, j);
+					if ((m2 >> j) & 1u) {
+						const uint32_t x = rdlane(sV, j);
 						uint32_t s = kSentinel, sf = 0;
 #pragma unroll
 						for (int k = 0; k < kHistChunks; ++k) {
@@ -332,9 +376,9 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 								if (m) { const uint32_t l = ffs64(m); s = 64u * k + l; sf = rdlane(hfR[k], l); }
 							}
 						}
-						if (s != kSentinel && sf == xf) {
-							const uint64_t e = src.extend(v0 + t, r0 + s, min(vl - (v0 + t), rl - (r0 + s)));
-							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; }
+						if (s != kSentinel && sf == rdlane(fVl, j)) {
+							const uint32_t e = src.extend(v0 + t, r0 + s, umin32(vl - (v0 + t), rl - (r0 + s)));
+							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s; ml = e; break; }
 						}
 					}
 				}
@@ -347,8 +391,8 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 						if (lane == 0) {   // bounded spin over the pool
 							const uint32_t n = a.n_tables;
 							for (uint32_t it = 0; it < (1u << 26) && got == 0xFFFFFFFFu; ++it) {
-								const uint32_t sl = (pair + it) % n;
-								if (atomicCAS(&a.table_locks[sl], 0u, 1u) == 0u) got = sl;
+								const uint32_t slx = (pair + it) % n;
+								if (atomicCAS(&a.table_locks[slx], 0u, 1u) == 0u) got = slx;
 								else if ((it % n) == n - 1) __builtin_amdgcn_s_sleep(8);
 							}
 						}
@@ -375,24 +419,25 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 						tab_insert(HR, hsR[k], tag, 64u * k + lane);
 					}
 				}
-				tab_insert(HV, sV, tag, (uint32_t)step);
-				tab_insert(HR, sR, tag, (uint32_t)step);
+				tab_insert(HV, sV, tag, step);
+				tab_insert(HR, sR, tag, step);
 				vm_drain();
-				const uint32_t c1 = cr ? tab_lookup(HV, sR, tag, (uint32_t)step) : kSentinel;
-				const uint32_t c2 = cv ? tab_lookup(HR, sV, tag, (uint32_t)step) : kSentinel;
-				const uint64_t any = __ballot(c1 != kSentinel || c2 != kSentinel);
-				for (uint32_t j = 0; j < nlive && !matched && any; ++j) {
-					if (!((any >> j) & 1)) continue;
-					const uint64_t t = 64ull * c + j;
+				const uint32_t c1 = cr ? tab_lookup(HV, sR, tag, step) : kSentinel;
+				const uint32_t c2 = cv ? tab_lookup(HR, sV, tag, step) : kSentinel;
+				uint64_t any = __ballot(c1 != kSentinel || c2 != kSentinel);
+				while (any) {
+					const uint32_t j = ffs64(any);
+					any &= any - 1;
+					const uint32_t t = b0 + j;
 					const uint32_t s1 = rdlane(c1, j);
 					if (s1 != kSentinel) {
-						const uint64_t e = src.extend(v0 + s1, r0 + t, min(vl - (v0 + s1), rl - (r0 + t)));
-						if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; }
+						const uint32_t e = src.extend(v0 + s1, r0 + t, umin32(vl - (v0 + s1), rl - (r0 + t)));
+						if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; break; }
 					}
 					const uint32_t s2 = rdlane(c2, j);
-					if (!matched && s2 != kSentinel) {
-						const uint64_t e = src.extend(v0 + t, r0 + s2, min(vl - (v0 + t), rl - (r0 + s2)));
-						if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; }
+					if (s2 != kSentinel) {
+						const uint32_t e = src.extend(v0 + t, r0 + s2, umin32(vl - (v0 + t), rl - (r0 + s2)));
+						if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; break; }
 					}
 				}
 			}
@@ -400,18 +445,28 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 		if (!matched) break;
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
-		if (nrec >= pp.rec_cap) { st = 7; break; }
-		if (lane == 0) {
-			rec[3u * nrec + 0] = (uint32_t)vm;
-			rec[3u * nrec + 1] = (uint32_t)rm;
-			rec[3u * nrec + 2] = (uint32_t)ml;
-		}
+		if (nrec >= rec_cap) { st = 7; break; }
+		const uint32_t k = nrec & 63u;
+		sv = lane == k ? vm : sv;
+		sr = lane == k ? rm : sr;
+		sl = lane == k ? ml : sl;
 		++nrec;
-		dsz += 13 + (vm > v0 ? 9 + (vm - v0) : 0);
+		if (k == 63) {   // 64 staged records -> one coalesced flush
+			uint32_t* o = rec + 3u * (nrec - 64 + lane);
+			o[0] = sv; o[1] = sr; o[2] = sl;
+		}
+		dsz += 13 + (vm > v0 ? 9 + (uint64_t)(vm - v0) : 0);
 		v0 = vm + ml;
 		r0 = rm + ml;
 	}
-	if (v0 < vl) dsz += 9 + (vl - v0);   // trailing ADD (:268-275)
+	if (v0 < vl) dsz += 9 + (uint64_t)(vl - v0);   // trailing ADD (:268-275)
+	{
+		const uint32_t k = nrec & 63u;   // flush the partial group
+		if (lane < k) {
+			uint32_t* o = rec + 3u * (nrec - k + lane);
+			o[0] = sv; o[1] = sr; o[2] = sl;
+		}
+	}
 
 	if (tslot >= 0 && lane == 0) {
 		__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -425,9 +480,10 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 	}
 }
 
-// p = 16, LDS windows (the hot configuration)
+// p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
 __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
+	__shared__ uint32_t bm[128];
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
@@ -435,39 +491,40 @@ __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	WinSrc src;
 	src.S[0] = a.ver + pd.v_off;
 	src.S[1] = a.ref + pd.r_off;
-	src.len[0] = pd.v_len;
-	src.len[1] = pd.r_len;
-	src.base[0] = src.base[1] = INT64_MIN / 2;   // nothing loaded yet
-	src.win = win;
+	src.len[0] = (uint32_t)pd.v_len;
+	src.len[1] = (uint32_t)pd.r_len;
+	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
+	src.win = (lds_u8*)win;
 	src.powc = a.powc;
 	uint64_t cA[4];
 	const uint32_t part = lane_id() & 3u;
 #pragma unroll
 	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
-	onepass_pair(src, a, pair, pd, pp, 16u, cA);
+	onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
 }
 
-// any seed length, bytes from HBM/L2
+// any seed length or alignment, bytes from HBM/L2
 template <int PF>
 __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
+	__shared__ uint32_t bm[128];
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	GlobalSrc<PF> src{a.ver + pd.v_off, a.ref + pd.r_off, PF > 0 ? (uint32_t)PF : a.p, a.powc};
 	const uint64_t cA[4] = {0, 0, 0, 0};
-	onepass_pair(src, a, pair, pd, pp, src.p, cA);
+	onepass_pair(src, a, pair, pd, pp, src.p, cA, bm);
 }
 
-// DG_ONEPASS_GLOBAL=1 selects the HBM-direct p=16 kernel (A/B measurements)
-static bool getenv_flag_global_src() {
+// DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B measurements)
+static bool force_global_src() {
 	const char* e = getenv("DG_ONEPASS_GLOBAL");
 	return e && e[0] == '1';
 }
 
-hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, hipStream_t st) {
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
 	if (a.n_pairs == 0) return hipSuccess;
-	if (p == 16 && !getenv_flag_global_src())
+	if (p == 16 && aligned16 && !force_global_src())
 		hipLaunchKernelGGL(onepass16_kernel, dim3(a.n_pairs), dim3(64), 0, st, a);
 	else if (p == 16)
 		hipLaunchKernelGGL(onepass_kernel<16>, dim3(a.n_pairs), dim3(64), 0, st, a);
