@@ -204,6 +204,95 @@ struct WinSrc {
 	__device__ uint64_t fpV(uint32_t pos) const { return fp16(0, pos); }
 	__device__ uint64_t fpR(uint32_t pos) const { return fp16(1, pos); }
 
+	// ── diagonal batch ──────────────────────────────────────────────────
+	// State (v0, r0) sits on a mismatch (V[v0] != R[r0]) left by the previous
+	// extension.  Let a_0 = 0 < a_1 < ... be the mismatch offsets along the
+	// diagonal (plus the stream end as a terminator) within the next 1 KiB.
+	// Epoch i starts at (v0+a_i, r0+a_i).  Its step 0 cannot match (first
+	// bytes differ).  If a_{i+1} - a_i >= 17, step 1's windows are equal, and
+	// step 1 resolves as the reference would iff
+	//   slotV0 != slotR1                          (lookup 1 finds s = 1), or
+	//   fpV0 != fpR1 and slotR0 != slotV1         (lookup 1's s = 0 fails
+	//                                              memcmp; lookup 2 finds s = 1)
+	// in which case the epoch emits ADD(1 byte) + COPY(a_i+1 .. a_{i+1}).
+	// Four lanes per epoch compute the four window slots; the first epoch
+	// that does not qualify ends the batch and goes through the exact path.
+	// Returns the number of epochs committed; *adv = offset of the new state.
+	__device__ uint32_t diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
+	                               uint64_t qmag, uint32_t* rec, uint32_t nrec, uint32_t rec_cap,
+	                               uint32_t* mlist, uint32_t* adv, uint32_t* npred) {
+		const uint32_t lane = lane_id();
+		const uint32_t lim = umin32(vl - v0, rl - r0);
+		*npred = 0;
+		*adv = 0;
+		// epoch 0 qualifies only if bytes 1..16 agree: check them first (cheap)
+		if (lim < 17) return 0;
+		ensure2(v0, r0, 24, true, true);
+		const uint32_t x0 = lane < 4 ? (rd4(0, v0 + 1 + 4 * lane) ^ rd4(1, r0 + 1 + 4 * lane)) : 0u;
+		if (__ballot(x0 != 0)) return 0;
+		ensure2(v0, r0, 1024 + 48, true, true);
+		// 1. mismatch bits of offsets [16*lane, 16*lane+16)
+		const uint32_t base = 16 * lane;
+		uint32_t bits = 0;
+#pragma unroll
+		for (uint32_t g = 0; g < 4; ++g) {
+			const uint32_t x = rd4(0, v0 + base + 4 * g) ^ rd4(1, r0 + base + 4 * g);
+			const uint32_t t = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // byte != 0
+			bits |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * g);
+		}
+		if (base + 16 > lim) {   // past the shorter stream: only its end terminates a match
+			bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
+			if (lim >= base && lim < base + 16) bits |= 1u << (lim - base);
+		}
+		// 2. ordered list of mismatch offsets (exclusive prefix of counts)
+		const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+		uint32_t incl = cnt;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) {
+			const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+			if (lane >= (uint32_t)d) incl += y;
+		}
+		uint32_t pos = incl - cnt;
+		const uint32_t total = rdlane(incl, 63);
+		for (uint32_t b = bits; b && pos < 64; b &= b - 1, ++pos) mlist[pos] = base + __builtin_ctz(b);
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		const uint32_t K = umin32(total, 64u);
+		const uint32_t E = K > 1 ? umin32(K - 1, 16u) : 0u;
+		*npred = E;
+		*adv = 0;
+		if (E == 0) return 0;
+		// 3. the four windows of each predicted epoch
+		const uint32_t i = lane >> 2, w = lane & 3u;
+		const bool act = i < E;
+		const uint32_t ai = act ? mlist[i] : 0u;
+		const uint32_t g = act ? mlist[i + 1] - ai : 0u;
+		const uint32_t s = w >> 1;
+		const uint64_t fp = fp16(s, (s ? r0 : v0) + ai + (w & 1u));
+		const uint32_t slot = (uint32_t)mod_q(fp, q, qmag);
+		const uint32_t fpl = (uint32_t)fp;
+		const uint32_t sV0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0x00, 0xF, 0xF, false);
+		const uint32_t sV1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0x55, 0xF, 0xF, false);
+		const uint32_t sR0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0xAA, 0xF, 0xF, false);
+		const uint32_t sR1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0xFF, 0xF, 0xF, false);
+		const uint32_t fV0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpl, 0x00, 0xF, 0xF, false);
+		const uint32_t fR1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpl, 0xFF, 0xF, 0xF, false);
+		const bool ok = act && g >= 17 && (sV0 != sR1 || (fV0 != fR1 && sR0 != sV1));
+		const uint64_t heads = 0x1111111111111111ull & ((E >= 16) ? ~0ull : ((1ull << (4 * E)) - 1ull));
+		const uint64_t bad = heads & ~__ballot(ok);
+		uint32_t f = bad ? (ffs64(bad) >> 2) : E;
+		if (nrec + f > rec_cap) f = 0;
+		// 4. commit epochs 0..f-1: ADD V[a_i] (1 byte) + COPY(a_i+1, a_{i+1}-a_i-1)
+		if (w == 0 && i < f) {
+			uint32_t* o = rec + 3u * (nrec + i);
+			o[0] = v0 + ai + 1;
+			o[1] = r0 + ai + 1;
+			o[2] = g - 1;
+		}
+		*adv = mlist[f];
+		return f;
+	}
+
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
 	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
 		const uint32_t lane = lane_id();
@@ -240,8 +329,6 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 	uint32_t nrec = 0;
 	uint64_t dsz = 26;   // header (25) + END
 	int32_t st = 0;
-	// COPY records staged in VGPRs (lane k holds record k mod 64)
-	uint32_t sv = 0, sr = 0, sl = 0;
 
 	int32_t tslot = -1;  // table tier state
 	uint32_t tag = 0;
@@ -250,10 +337,27 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 
 	uint32_t v0 = 0, r0 = 0;
 	bool scanning = vl > 0;
+	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
 	while (scanning) {
 		// no match is possible once either stream cannot supply a window at
 		// the epoch start (the reference keeps scanning the other, :102-104)
 		if (v0 + p > vl || r0 + p > rl) break;
+		if constexpr (Src::kPhaseA) {
+			if (at_mismatch) {
+				uint32_t adv = 0, npred = 0;
+				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, rec, nrec, rec_cap, bm,
+				                                      &adv, &npred));
+				if (f) {
+					adv = uni(adv);
+					nrec += f;
+					dsz += 23ull * f;   // per epoch: ADD 9+1 B, COPY 13 B
+					v0 += adv;
+					r0 += adv;
+					if (f == uni(npred)) continue;   // all predicted: next batch
+					if (v0 + p > vl || r0 + p > rl) break;
+				}
+			}
+		}
 		const uint32_t nv = vl - p - v0 + 1;   // steps with a V window
 		const uint32_t nr = rl - p - r0 + 1;   // steps with an R window
 		const uint32_t nlive = umax32(nv, nr);
@@ -446,27 +550,14 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
 		if (nrec >= rec_cap) { st = 7; break; }
-		const uint32_t k = nrec & 63u;
-		sv = lane == k ? vm : sv;
-		sr = lane == k ? rm : sr;
-		sl = lane == k ? ml : sl;
+		if (lane < 3) rec[3u * nrec + lane] = lane == 0 ? vm : (lane == 1 ? rm : ml);
 		++nrec;
-		if (k == 63) {   // 64 staged records -> one coalesced flush
-			uint32_t* o = rec + 3u * (nrec - 64 + lane);
-			o[0] = sv; o[1] = sr; o[2] = sl;
-		}
 		dsz += 13 + (vm > v0 ? 9 + (uint64_t)(vm - v0) : 0);
 		v0 = vm + ml;
 		r0 = rm + ml;
+		at_mismatch = true;
 	}
 	if (v0 < vl) dsz += 9 + (uint64_t)(vl - v0);   // trailing ADD (:268-275)
-	{
-		const uint32_t k = nrec & 63u;   // flush the partial group
-		if (lane < k) {
-			uint32_t* o = rec + 3u * (nrec - k + lane);
-			o[0] = sv; o[1] = sr; o[2] = sl;
-		}
-	}
 
 	if (tslot >= 0 && lane == 0) {
 		__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
