@@ -227,8 +227,9 @@ class EncodePlan:
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)
 
-    def set_timing(self, on: bool = True):
-        self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(on)), "set_timing")
+    def set_timing(self, slots: int = 1):
+        """Record per-stage events for the next runs (ring of `slots` sets)."""
+        self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(slots)), "set_timing")
 
     def stage_times(self):
         ms = (C.c_float * 8)()

@@ -296,14 +296,19 @@ struct dg_encode_plan {
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
 	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_cand;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
+	// fork/join of the CRC kernels onto a side stream
+	hipStream_t side = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	// timing
 	bool timing = false;
-	hipEvent_t ev[8] = {};
-	float stage_ms[8] = {};
-	int n_stages = 0;
+	// timing: `slots` sets of kTimingEvents events, one set per run (ring)
+	std::vector<hipEvent_t> ev;
+	uint32_t slots = 0, runs = 0;
+	hipEvent_t* cur = nullptr;   // event set of the run being enqueued
 };
 
-static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize"};
+static const char* kStageNames[] = {"crc64", "diff", "scan+join", "serialize", "total"};
 
 extern "C" {
 
@@ -446,6 +451,17 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		delete P;
 		return set_err(ctx, DG_ERR_HIP, "plan upload failed: %s", hipGetErrorString(e));
 	}
+	const char* sc = getenv("DG_SERIAL_CRC");
+	P->serial_crc = sc && sc[0] == '1';
+	if (!P->serial_crc) {
+		e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
+		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
+		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_join, hipEventDisableTiming);
+		if (e != hipSuccess) {
+			dg_encode_plan_destroy(P);
+			return set_err(ctx, DG_ERR_HIP, "side stream creation failed: %s", hipGetErrorString(e));
+		}
+	}
 	*out = P;
 	return DG_OK;
 }
@@ -459,24 +475,46 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 	return P ? P->d_nrec.as<uint32_t>() : nullptr;
 }
 
-int dg_encode_plan_set_timing(dg_encode_plan_t* P, int enable) {
-	if (!P) return DG_ERR_INVALID_ARG;
-	if (enable && !P->timing) {
-		for (int i = 0; i < 5; ++i)
-			if (hipEventCreate(&P->ev[i]) != hipSuccess) return DG_ERR_HIP;
+constexpr int kTimingEvents = 6;
+
+int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
+	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
+	hipSetDevice(P->ctx->device);
+	if ((uint32_t)slots > P->slots) {
+		for (auto& e : P->ev) hipEventDestroy(e);
+		P->ev.assign((size_t)kTimingEvents * slots, nullptr);
+		for (auto& e : P->ev)
+			if (hipEventCreate(&e) != hipSuccess) {
+				e = nullptr;
+				return set_err(P->ctx, DG_ERR_HIP, "hipEventCreate failed");
+			}
+		P->slots = (uint32_t)slots;
 	}
-	P->timing = enable != 0;
+	P->timing = slots > 0;
+	P->runs = 0;
 	return DG_OK;
 }
 
+// Per-run events: 0/1 around the CRC kernels (side stream), 2/3 around the
+// differencing kernel, 4 after the scan + CRC join, 5 after serialisation.
+// Returns the mean over the runs recorded since set_timing (at most `slots`).
 int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
-	if (!P || !P->timing) return 0;
-	if (hipEventSynchronize(P->ev[4]) != hipSuccess) return 0;
+	if (!P || !P->slots || !P->runs) return 0;
+	const uint32_t used = std::min(P->runs, P->slots);
+	const int pairs[5][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}};
+	double acc[5] = {};
+	for (uint32_t s = 0; s < used; ++s) {
+		hipEvent_t* e = &P->ev[(size_t)kTimingEvents * s];
+		if (hipEventSynchronize(e[5]) != hipSuccess) return 0;
+		for (int k = 0; k < 5; ++k) {
+			float t = 0;
+			hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]);
+			acc[k] += t;
+		}
+	}
 	int k = 0;
-	for (; k < 4 && k < n; ++k) {
-		float t = 0;
-		hipEventElapsedTime(&t, P->ev[k], P->ev[k + 1]);
-		if (ms) ms[k] = t;
+	for (; k < 5 && k < n; ++k) {
+		if (ms) ms[k] = (float)(acc[k] / used);
 		if (names) names[k] = kStageNames[k];
 	}
 	return k;
@@ -494,9 +532,15 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		return set_err(ctx, DG_ERR_INVALID_ARG, "arena base pointers must be 16-byte aligned");
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
 
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[0], st));
-	// 1. CRC-64/XZ of every R (even spans) and V (odd spans)
-	{
+	// The CRC-64/XZ of every R (even spans) and V (odd spans) shares nothing
+	// with the differencing kernel until the serialiser, so it runs on a
+	// forked side stream.  The differencing kernel is enqueued first so its
+	// (long, latency-bound) waves are resident before the CRC waves fill the
+	// issue slots they leave idle.
+	hipStream_t cs = P->serial_crc ? st : P->side;
+	if (P->timing) P->cur = &P->ev[(size_t)kTimingEvents * (P->runs++ % P->slots)];
+	auto run_crc = [&]() -> int {
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[0], cs));
 		CrcArgs a{};
 		a.arena[0] = d_ref;
 		a.arena[1] = d_ver;
@@ -509,11 +553,13 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
-		HIPCHK(ctx, launch_crc(a, st));
-	}
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[1], st));
-	// 2. differencing -> COPY records + per-pair delta sizes
-	{
+		HIPCHK(ctx, launch_crc(a, cs));
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[1], cs));
+		return DG_OK;
+	};
+	// differencing -> COPY records + per-pair delta sizes
+	auto run_diff = [&]() -> int {
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[2], st));
 		EncodeArgs a{};
 		a.ref = d_ref;
 		a.ver = d_ver;
@@ -536,11 +582,24 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 		else
 			HIPCHK(ctx, launch_correcting(a, a.p, st));
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[3], st));
+		return DG_OK;
+	};
+	int rc;
+	if (P->serial_crc) {
+		if ((rc = run_crc()) != DG_OK) return rc;
+		if ((rc = run_diff()) != DG_OK) return rc;
+	} else {
+		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
+		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
+		if ((rc = run_diff()) != DG_OK) return rc;
+		if ((rc = run_crc()) != DG_OK) return rc;
+		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
 	}
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[2], st));
 	// 3. exclusive scan of sizes -> packed offsets
 	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[3], st));
+	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
 	// 4. serialise
 	{
 		SerArgs s{};
@@ -557,7 +616,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		s.n_pairs = P->n;
 		HIPCHK(ctx, launch_serialize(s, st));
 	}
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->ev[4], st));
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
 	return DG_OK;
 }
 
@@ -565,8 +624,12 @@ void dg_encode_plan_destroy(dg_encode_plan_t* P) {
 	if (!P) return;
 	hipSetDevice(P->ctx->device);
 	hipStreamSynchronize(P->ctx->stream);
+	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
+	if (P->ev_fork) hipEventDestroy(P->ev_fork);
+	if (P->ev_join) hipEventDestroy(P->ev_join);
+	if (P->side) hipStreamDestroy(P->side);
 	delete P;
 }
 

@@ -235,21 +235,34 @@ __global__ __launch_bounds__(256) void crc_segments_kernel(CrcArgs a) {
 	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
 
 	uint64_t reg = 0;
-	for (uint32_t w = 0; w < kCrcLaneBytes; w += 16) {
-		const uintptr_t addr = cs + w;
-		// words wholly before the data are virtual zeros: no-ops on a zero register
-		if ((intptr_t)(addr + 16 - a0) <= 0) continue;
-		const ulonglong2 x = *reinterpret_cast<const ulonglong2*>(addr);
-		uint64_t lo = x.x, hi = x.y;
-		const int f = (int)((intptr_t)start - (intptr_t)addr);   // first data byte index
-		const int l = (int)((intptr_t)end - (intptr_t)addr);     // one past last
-		lo &= byte_mask(f, l);
-		hi &= byte_mask(f - 8, l - 8);
-		// init = ~0: invert the span's first 8 bytes
-		lo ^= byte_mask(f, f + 8);
-		hi ^= byte_mask(f - 8, f);
-		reg = slice8(reg ^ lo, T);
-		reg = slice8(reg ^ hi, T);
+	constexpr int kPf = 8;   // 16-byte loads in flight per lane
+	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
+		ulonglong2 xs[kPf];
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const uintptr_t addr = cs + w0 + 16 * u;
+			// words wholly before the data are virtual zeros: no-ops on a zero register
+			if ((intptr_t)(addr + 16 - a0) > 0) xs[u] = *reinterpret_cast<const ulonglong2*>(addr);
+			else xs[u] = make_ulonglong2(0, 0);
+		}
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const uintptr_t addr = cs + w0 + 16 * u;
+			uint64_t lo = xs[u].x, hi = xs[u].y;
+			const intptr_t f = (intptr_t)start - (intptr_t)addr;   // first data byte index
+			const intptr_t l = (intptr_t)end - (intptr_t)addr;     // one past last
+			if (f > -8 || l < 16) {   // only the span's edges need masking
+				const int fc = (int)max(min(f, (intptr_t)24), (intptr_t)-8);
+				const int lc = (int)max(min(l, (intptr_t)24), (intptr_t)-8);
+				lo &= byte_mask(fc, lc);
+				hi &= byte_mask(fc - 8, lc - 8);
+				// init = ~0: invert the span's first 8 bytes
+				lo ^= byte_mask(fc, fc + 8);
+				hi ^= byte_mask(fc - 8, fc);
+			}
+			reg = slice8(reg ^ lo, T);
+			reg = slice8(reg ^ hi, T);
+		}
 	}
 	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
 	const uint64_t* L = T + 8 * 256;

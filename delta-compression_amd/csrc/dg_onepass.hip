@@ -417,7 +417,6 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 		for (uint32_t c = 0; !matched; ++c) {
 			const uint32_t b0 = 64 * c;
 			if (b0 >= nlive) { scanning = false; break; }   // both streams exhausted
-			const uint32_t nl = umin32(64u, nlive - b0);
 			const uint32_t step = b0 + lane;
 			const bool cv = step < nv, cr = step < nr;
 			src.chunk(v0 + b0, r0 + b0, b0 < nv, b0 < nr);

@@ -159,11 +159,15 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
                        uint8_t *d_out, uint64_t out_cap,
                        uint64_t *d_offsets, int32_t *d_status,
                        void *stream);
-/* Optional per-stage timing with HIP events on the run stream.  When enabled
- * each run records events around every kernel; dg_encode_plan_stage_times
- * fills up to `n` stage durations (ms) of the last run and their names.
- * Returns the number of stages. */
-int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int enable);
+/* Optional per-stage timing with HIP events on the streams the kernels run on
+ * (the CRC kernels run on a plan-owned side stream forked from / joined to
+ * the run stream).  dg_encode_plan_set_timing(plan, slots) with slots > 0
+ * makes every run record its events into one of `slots` event sets (a ring;
+ * 0 disables) and resets the run count; dg_encode_plan_stage_times fills up to
+ * `n` stage durations (ms), averaged over the last min(runs, slots) runs, and
+ * their names ("crc64", "diff", "scan+join", "serialize", "total").  Returns
+ * the number of stages.  No host synchronisation happens until stage_times. */
+int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
                                const char **names, int n);
 /* Per-pair command statistics of the last run (device pointers owned by the
