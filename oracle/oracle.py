@@ -183,7 +183,20 @@ class Reference:
         u8p, sz = C.POINTER(C.c_uint8), C.c_size_t
         L.ref_encode_pair.restype = sz
         L.ref_encode_pair.argtypes = [C.c_int, u8p, sz, u8p, sz, sz, sz, sz, sz, C.POINTER(u8p)]
+        L.ref_encode_pair_inplace.restype = sz
+        L.ref_encode_pair_inplace.argtypes = [C.c_int, u8p, sz, u8p, sz, sz, sz, C.c_int,
+                                              C.POINTER(u8p)]
         L.ref_free.argtypes = [C.c_void_p]
+
+    def encode_inplace(self, algo: int, R: bytes, V: bytes, p: int = SEED_LEN,
+                       q: int = TABLE_SIZE, policy: int = 0) -> bytes:
+        """main.c encode --inplace [--policy localmin|constant]: an in-place delta."""
+        out = C.POINTER(C.c_uint8)()
+        n = self.L.ref_encode_pair_inplace(algo, _buf(R), len(R), _buf(V), len(V), p, q, policy,
+                                           C.byref(out))
+        res = C.string_at(out, n)
+        self.L.ref_free(out)
+        return res
 
     def encode(self, algo: int, R: bytes, V: bytes, p: int = SEED_LEN, q: int = TABLE_SIZE,
                buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE) -> bytes:

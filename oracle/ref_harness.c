@@ -48,6 +48,30 @@ size_t ref_encode_pair(int algo, const uint8_t *r, size_t r_len,
 	return b.len;
 }
 
+/* main.c:257-292 with --inplace: delta_make_inplace (policy 0 = localmin,
+ * 1 = constant) replaces delta_place_commands; the header flag is set.  Used
+ * to produce the in-place command streams the decode tests and the C5
+ * decode bench replay. */
+size_t ref_encode_pair_inplace(int algo, const uint8_t *r, size_t r_len,
+                               const uint8_t *v, size_t v_len, size_t p,
+                               size_t q, int policy, uint8_t **out)
+{
+	uint8_t sc[DELTA_CRC_SIZE], dc[DELTA_CRC_SIZE];
+	delta_diff_options_t o = DELTA_DIFF_OPTIONS_DEFAULT;
+	o.p = p;
+	o.q = q;
+	delta_crc64_xz(r, r_len, sc);
+	delta_crc64_xz(v, v_len, dc);
+	delta_commands_t cmds = delta_diff((delta_algorithm_t)algo, r, r_len, v, v_len, &o);
+	delta_placed_commands_t placed =
+	    delta_make_inplace(r, r_len, &cmds, (delta_cycle_policy_t)policy);
+	delta_buffer_t b = delta_encode(&placed, true, v_len, sc, dc);
+	delta_placed_commands_free(&placed);
+	delta_commands_free(&cmds);
+	*out = b.data;
+	return b.len;
+}
+
 void ref_free(void *p) { free(p); }
 
 #ifdef REF_BENCH_MAIN

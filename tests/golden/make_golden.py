@@ -85,6 +85,41 @@ def main():
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {len(out['cases'])} cases to {path}")
+    make_inplace(ref, orc)
+
+
+def make_inplace(ref, orc):
+    """In-place deltas (main.c encode --inplace: delta_make_inplace +
+    delta_encode(inplace=true)) with their bytes inline, so the decode tests
+    can replay them on the GPU box where the reference is absent."""
+    out = {"generator": "reference src/c via oracle/_ref (ref_encode_pair_inplace)", "cases": []}
+
+    def add(name, algo, R, V, q, policy, **extra):
+        d = ref.encode_inplace(algo, R, V, p=16, q=q, policy=policy)
+        out["cases"].append(dict(name=name, algo=algo, q=q, policy=policy, r_sha256=sha(R),
+                                 v_sha256=sha(V), r_len=len(R), v_len=len(V),
+                                 delta_len=len(d), delta_hex=d.hex(), **extra))
+
+    for name, R, V, p, q in small_cases():
+        if p != 16:
+            continue
+        for policy in (0, 1):
+            add(f"{name}_pol{policy}", O.ONEPASS, R, V, q, policy, kind="small")
+    for i in range(4):
+        R, V = orc.synth_pair(0xC2000000 + i, 65536, 655)
+        add(f"c2_{i}", O.ONEPASS, R, V, 1, i & 1, kind="synth_edits", seed=0xC2000000 + i,
+            pair_len=65536, n_edits=655)
+    # shifted content: blocks move both ways, so the CRWI graph has cycles
+    for i in range(2):
+        nb = 8 + i
+        R, V = orc.synth_transpose(0xC4000000 + i, nb, 65536 // nb, 50)
+        for policy in (0, 1):
+            add(f"transpose_{i}_pol{policy}", O.CORRECTING, R, V, 1, policy,
+                kind="synth_transpose", seed=0xC4000000 + i, num_blocks=nb, mean=65536 // nb, pct=50)
+    path = os.path.join(HERE, "golden_inplace.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    print(f"wrote {len(out['cases'])} in-place cases to {path}")
 
 
 if __name__ == "__main__":

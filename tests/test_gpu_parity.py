@@ -233,3 +233,20 @@ def test_cli_encode_decode_vs_reference(tmp_path, orc):
     bad = subprocess.run([cli, "decode", str(vp), str(tmp_path / "d"), str(tmp_path / "out2")],
                          capture_output=True, text=True)
     assert bad.returncode == 1 and "source file does not match delta" in bad.stderr
+
+
+# ── in-place deltas minted by the reference (delta_make_inplace) ─────────
+
+def test_golden_inplace_decode_on_device(dg, ctx, orc):
+    """Every reference in-place delta (tests/golden/golden_inplace.json,
+    both cycle policies, onepass and correcting) replays on the device into
+    a max(|R|, |V|) buffer in command order (apply.c:253-284) and passes the
+    on-device src/dst CRC checks."""
+    import json
+    from test_oracle import inplace_inputs
+    here = os.path.dirname(os.path.abspath(__file__))
+    cases = json.load(open(os.path.join(here, "golden", "golden_inplace.json")))["cases"]
+    for c in cases:
+        R, V = inplace_inputs(orc, c)
+        d = bytes.fromhex(c["delta_hex"])
+        assert dg.decode(R, d, ctx=ctx) == V, c["name"]

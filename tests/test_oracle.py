@@ -126,3 +126,31 @@ def test_decode_errors(orc):
     assert orc.decode(R, bytes(bad), ignore_hash=True)[1] == V
     assert orc.decode(R, b"NOPE" + d[4:])[0] == 8
     assert orc.decode(R, d[:30])[0] == 8
+
+
+# ── in-place deltas (main.c encode --inplace), minted from the reference ──
+
+GOLDEN_INPLACE = json.load(open(os.path.join(HERE, "golden", "golden_inplace.json")))["cases"]
+
+
+def inplace_inputs(orc, case):
+    kind = case["kind"]
+    if kind == "small":
+        m = {c[0]: c for c in small_cases()}
+        base = case["name"].rsplit("_pol", 1)[0]
+        return m[base][1], m[base][2]
+    if kind == "synth_edits":
+        return orc.synth_pair(case["seed"], case["pair_len"], case["n_edits"])
+    return orc.synth_transpose(case["seed"], case["num_blocks"], case["mean"], case["pct"])
+
+
+@pytest.mark.parametrize("case", GOLDEN_INPLACE, ids=lambda c: c["name"])
+def test_golden_inplace_oracle_decode(orc, case):
+    """The oracle's decode (apply.c:253-284 in-place replay) rebuilds V from
+    every reference in-place delta, CRCs checked."""
+    R, V = inplace_inputs(orc, case)
+    assert _sha(R) == case["r_sha256"] and _sha(V) == case["v_sha256"]
+    d = bytes.fromhex(case["delta_hex"])
+    assert d[4] == 1, "in-place flag"
+    rc, out = orc.decode(R, d)
+    assert rc == 0 and out == V
