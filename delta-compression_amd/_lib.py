@@ -12,7 +12,9 @@ import threading
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libdeltagpu.so")
+# DG_LIB_VARIANT=prof selects the profiling build (make prof); never a CPU path
+_VARIANT = os.environ.get("DG_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, "lib", "libdeltagpu%s.so" % ("_" + _VARIANT if _VARIANT else ""))
 
 ALGO_GREEDY, ALGO_ONEPASS, ALGO_CORRECTING = 0, 1, 2
 SEED_LEN = 16

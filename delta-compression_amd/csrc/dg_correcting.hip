@@ -1,0 +1,363 @@
+// dg_correcting.hip — correcting differencing on gfx950
+// (src/c/correcting.c:81-495, hash-table path; restated in oracle/delta_oracle.c
+// or_diff_correcting).
+//
+// Two kernels per batch:
+//
+//   correcting_build_kernel   the checkpointed R index (correcting.c:164-198).
+//       Every R seed a whose fingerprint passes the checkpoint test
+//       (fp mod |F|) mod m == k stores itself at slot i = (fp mod |F|) / m
+//       when i < cap, FIRST FOUND WINS — i.e. the smallest offset per slot, so
+//       the build is an order-free atomicMin over all seeds in parallel.  The
+//       grid is (pair, 4 KiB of R); each lane rolls the hash over 16
+//       consecutive seeds.  The table stores offsets only: the reference's
+//       stored-fingerprint test (`h[i].fp == fp`, :268) is implied by the
+//       memcmp that follows it, since equal bytes have equal fingerprints.
+//
+//   correcting_scan_kernel    the V scan with forward/backward extension and
+//       the lookback buffer's tail correction (correcting.c:229-468), one
+//       wave64 per pair.  The scan advances one position at a time until a
+//       verified match, so a chunk of 64 consecutive positions is tested at
+//       once (lane = position) and the first verified lane is the reference's
+//       next match.  Extensions are wave-parallel, 16 bytes per lane per
+//       step.  The lookback buffer (a ring of buf_cap entries) lives in LDS
+//       and is driven by wave-uniform scalar code; entries that leave it are
+//       final and become COPY records (ADDs are the gaps between COPYs, as
+//       for onepass, so the serialiser is shared).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dg_device.h"
+#include "dg_devutil.h"
+
+namespace dg {
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kBuildSeedsPerLane = 16;
+constexpr uint32_t kBuildBlock = 256;
+constexpr uint32_t kBuildSeedsPerBlock = kBuildSeedsPerLane * kBuildBlock;   // 4096
+
+__device__ __forceinline__ uint32_t umin_(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+__device__ __forceinline__ uint64_t fold61c(uint64_t lo, uint64_t hi) {
+	// lo + hi * 2^32 mod (2^61 - 1), lo < 2^48, hi < 2^45
+	return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
+}
+
+// x * c mod M for x < 2^61 and c < 2^32
+__device__ __forceinline__ uint64_t mulsmall61(uint64_t x, uint32_t c) {
+	return fold61c((x & 0xFFFFFFFFull) * c, (x >> 32) * c);
+}
+
+// checkpoint class k: fingerprint of V[|V|/2 .. +p) (correcting.c:131-136),
+// bytes past |V| read as zero (the reference's out-of-bounds read, see
+// oracle/delta_oracle.c), reduced mod |F| then mod m.
+__device__ uint64_t checkpoint_class(const uint8_t* V, uint64_t vl, uint32_t p,
+                                     const PairPlanDev& pp) {
+	if (vl < p) return 0;
+	uint64_t h = 0;
+	for (uint32_t j = 0; j < p; ++j) {
+		const uint64_t at = vl / 2 + j;
+		h = mod_m61(mulsmall61(h, (uint32_t)kBase) + (at < vl ? V[at] : 0));
+	}
+	return mod_q(h, pp.f_size, pp.f_magic) % pp.m;
+}
+
+// f = fp mod |F|; passes iff f mod m == k; slot = f / m
+__device__ __forceinline__ bool checkpoint_slot(uint64_t fp, const PairPlanDev& pp, uint64_t k,
+                                                uint32_t* slot) {
+	const uint64_t f = mod_q(fp, pp.f_size, pp.f_magic);
+	uint64_t i, r;
+	if (pp.m == 1) {
+		i = f;
+		r = 0;
+	} else {
+		i = __umul64hi(f, pp.m_magic);
+		r = f - i * pp.m;
+		if (r >= pp.m) { r -= pp.m; ++i; }
+		if (r >= pp.m) { r -= pp.m; ++i; }
+	}
+	*slot = (uint32_t)i;
+	return r == k && i < pp.q;
+}
+
+// 4 bytes at an arbitrary address, from the aligned dwords that hold them
+__device__ __forceinline__ uint32_t ld4u(const uint8_t* p) {
+	const uintptr_t a = (uintptr_t)p;
+	const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+	const uint32_t s = (uint32_t)(a & 3);
+	const uint32_t w0 = w[0];
+	const uint32_t w1 = s ? w[1] : 0u;
+	return __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+
+// number of equal leading bytes of a[0..) and b[0..), at most lim; 1 KiB per
+// wave step (16 bytes per lane)
+__device__ uint32_t ext_fwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
+	const uint32_t lane = lane_id();
+	uint32_t ml = 0;
+	while (ml < lim) {
+		const uint32_t base = ml + 16 * lane;
+		uint32_t bad = 16;
+		if (base < lim) {
+			const uint32_t n = umin_(16u, lim - base);
+#pragma unroll
+			for (int g = 0; g < 4; ++g) {
+				if (bad == 16 && 4u * g < n) {
+					const uint32_t left = n - 4u * g;
+					if (left >= 4) {
+						const uint32_t x = ld4u(a + base + 4 * g) ^ ld4u(b + base + 4 * g);
+						if (x) bad = 4u * g + ((uint32_t)__builtin_ctz(x) >> 3);
+					} else {   // the last bytes before lim: no read past them
+						uint32_t e = left;
+						for (uint32_t t = 0; t < left; ++t)
+							if (e == left && a[base + 4 * g + t] != b[base + 4 * g + t]) e = t;
+						bad = 4u * g + e;   // == n when all equal: a mismatch at lim
+					}
+				}
+			}
+		}
+		const uint64_t m = __ballot(bad < 16);
+		if (m) {
+			const uint32_t f = ffs64(m);
+			return umin_(lim, ml + 16 * f + rdlane(bad, f));
+		}
+		ml += 1024;
+	}
+	return lim;
+}
+
+// number of equal bytes going backwards: a[-1] == b[-1], a[-2] == b[-2], ...,
+// at most lim
+__device__ uint32_t ext_bwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
+	const uint32_t lane = lane_id();
+	uint32_t ml = 0;
+	while (ml < lim) {
+		// lane covers back-offsets [ml + 16*lane, +16): bytes a[-(off+1)]
+		const uint32_t base = ml + 16 * lane;
+		uint32_t bad = 16;
+		if (base < lim) {
+			const uint32_t n = umin_(16u, lim - base);
+#pragma unroll
+			for (int g = 0; g < 4; ++g) {
+				if (bad == 16 && 4u * g < n) {
+					const uint32_t left = n - 4u * g;
+					if (left >= 4) {
+						// the 4 bytes at back-offsets base+4g .. +3; byte 3 is the nearest
+						const uint32_t o = base + 4 * g + 4;
+						const uint32_t x = ld4u(a - o) ^ ld4u(b - o);
+						if (x) bad = 4u * g + ((uint32_t)__builtin_clz(x) >> 3);
+					} else {   // the last bytes before lim: no read beyond them
+						uint32_t e = left;
+						for (uint32_t t = 0; t < left; ++t) {
+							const uint32_t d = base + 4 * g + t + 1;
+							if (e == left && *(a - d) != *(b - d)) e = t;
+						}
+						bad = 4u * g + e;
+					}
+				}
+			}
+		}
+		const uint64_t m = __ballot(bad < 16);
+		if (m) {
+			const uint32_t f = ffs64(m);
+			return umin_(lim, ml + 16 * f + rdlane(bad, f));
+		}
+		ml += 1024;
+	}
+	return lim;
+}
+
+}  // namespace
+
+// ───────────────────────────── build ──────────────────────────────────────
+
+__global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a) {
+	__shared__ uint64_t ob[256];   // x * 263^(p-1) mod M: the byte leaving the window
+	__shared__ uint64_t kcls;
+	const uint32_t pair = blockIdx.x;
+	const PairDev pd = a.pairs[pair];
+	const PairPlanDev pp = a.pplan[pair];
+	const uint32_t p = a.p;
+	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
+	const uint64_t blk0 = (uint64_t)blockIdx.y * kBuildSeedsPerBlock;
+	if (blk0 >= seeds || pd.v_len == 0) return;
+	const uint8_t* R = a.ref + pd.r_off;
+	const uint64_t top = a.powc[0];
+	{
+		const uint32_t x = threadIdx.x;
+		ob[x] = fold61c((uint64_t)x * (uint32_t)top, (uint64_t)x * (uint32_t)(top >> 32));
+	}
+	if (threadIdx.x == 0) kcls = checkpoint_class(a.ver + pd.v_off, pd.v_len, p, pp);
+	__syncthreads();
+	const uint64_t k = kcls;
+	uint32_t* H = a.ctab + pp.tab_base;
+
+	const uint64_t s0 = blk0 + (uint64_t)threadIdx.x * kBuildSeedsPerLane;
+	if (s0 >= seeds) return;
+	const uint32_t cnt = (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane);
+	uint64_t fp = window_fp<0>(R + s0, p, a.powc);
+	for (uint32_t j = 0; j < cnt; ++j) {
+		if (j) {   // roll: (fp - R[a-1] * 263^(p-1)) * 263 + R[a-1+p]   (hash.c:62-98)
+			const uint64_t s = s0 + j;
+			const uint64_t t = mod_m61(fp + kMersenne - ob[R[s - 1]]);
+			fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + R[s - 1 + p], (t >> 32) * (uint32_t)kBase);
+		}
+		uint32_t slot;
+		if (checkpoint_slot(fp, pp, k, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
+	}
+}
+
+// ───────────────────────────── scan ───────────────────────────────────────
+
+struct RingEnt {
+	uint32_t vs, ve, r_off, kind;   // kind: 1 COPY, 2 ADD
+};
+
+__global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
+	extern __shared__ RingEnt ring[];   // buf_cap + 1 entries
+	const uint32_t pair = blockIdx.x;
+	const uint32_t lane = lane_id();
+	const PairDev pd = a.pairs[pair];
+	const PairPlanDev pp = a.pplan[pair];
+	const uint32_t p = a.p;
+	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
+	const uint8_t* V = a.ver + pd.v_off;
+	const uint8_t* R = a.ref + pd.r_off;
+	const uint32_t* H = a.ctab + pp.tab_base;
+	const uint32_t bc = uni(a.buf_cap ? a.buf_cap : 1u);
+	const uint32_t rcap = bc + 1;
+	const uint32_t rec_cap = uni(pp.rec_cap);
+	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
+
+	uint32_t nrec = 0, head = 0, n = 0;
+	uint64_t dsz = 26;   // header + END
+	int32_t st = 0;
+
+	// the oldest buffer entry leaves for the output when the buffer is full
+	// (correcting.c:603-613)
+	auto emit_oldest_if_full = [&]() {
+		if (n >= bc) {
+			const RingEnt o = ring[head];
+			if (o.kind == 1) {
+				if (nrec >= rec_cap) st = 7;
+				else if (lane < 3) rec[3u * nrec + lane] = lane == 0 ? o.vs : (lane == 1 ? o.r_off : o.ve - o.vs);
+				++nrec;
+				dsz += 13;
+			} else {
+				dsz += 9ull + (o.ve - o.vs);
+			}
+			head = head + 1 == rcap ? 0 : head + 1;
+			--n;
+		}
+	};
+	auto push = [&](uint32_t kind, uint32_t vs_, uint32_t ve_, uint32_t r_off) {
+		uint32_t at = head + n;
+		if (at >= rcap) at -= rcap;
+		__builtin_amdgcn_wave_barrier();
+		if (lane == 0) ring[at] = RingEnt{vs_, ve_, r_off, kind};
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		++n;
+	};
+
+	if (vl > 0) {
+		const uint64_t k = uni64(checkpoint_class(V, vl, p, pp));
+		uint32_t vc = 0, vs = 0;
+		while (st == 0 && vc + p <= vl) {
+			// ── positions vc .. vc+63: fingerprint, checkpoint, lookup, memcmp ──
+			const uint32_t pos = vc + lane;
+			bool hit = false;
+			uint32_t off = kNone;
+			if (pos + p <= vl) {
+				const uint64_t fp = window_fp<0>(V + pos, p, a.powc);
+				uint32_t slot;
+				if (checkpoint_slot(fp, pp, k, &slot)) {
+					off = H[slot];
+					if (off != kNone) {   // correcting.c:268-285: verify the seed bytes
+						hit = true;
+						for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
+					}
+				}
+			}
+			const uint64_t M = __ballot(hit);
+			if (!M) { vc += 64; continue; }
+			const uint32_t jf = ffs64(M);
+			vc = uni(vc + jf);
+			const uint32_t ro = uni(rdlane(off, jf));
+			// ── extensions (correcting.c:293-303) ──
+			const uint32_t fwd = p + uni(ext_fwd(V + vc + p, R + ro + p, umin_(vl - vc - p, rl - ro - p)));
+			const uint32_t bwd = uni(ext_bwd(V + vc, R + ro, umin_(vc, ro)));
+			const uint32_t vm = vc - bwd, rm = ro - bwd, mend = vm + bwd + fwd;
+			if (vs <= vm) {
+				// 6a: the match lies in the unencoded suffix (correcting.c:316-363)
+				if (vs < vm) { emit_oldest_if_full(); push(2, vs, vm, 0); }
+				emit_oldest_if_full();
+				push(1, vm, mend, rm);
+			} else {
+				// 6b: tail correction (correcting.c:364-445)
+				uint32_t eff = vs;
+				while (n > 0) {
+					uint32_t at = head + n - 1;
+					if (at >= rcap) at -= rcap;
+					const RingEnt t = ring[at];
+					if (t.vs >= vm && t.ve <= mend) {   // wholly absorbed
+						eff = umin_(eff, t.vs);
+						--n;
+						continue;
+					}
+					if (t.ve > vm && t.vs < vm && t.kind == 2) {   // trim the ADD
+						__builtin_amdgcn_wave_barrier();
+						if (lane == 0) ring[at].ve = vm;
+						__builtin_amdgcn_s_waitcnt(0xc07f);
+						__builtin_amdgcn_wave_barrier();
+						eff = umin_(eff, vm);
+					}
+					break;
+				}
+				if (mend > eff) {
+					emit_oldest_if_full();
+					push(1, eff, mend, rm + (eff - vm));
+				}
+			}
+			vs = mend;
+			vc = mend;   // correcting.c:448
+		}
+		// flush the buffer (correcting.c:452-460) and the trailing ADD (:461-468)
+		while (n > 0) {
+			const RingEnt o = ring[head];
+			if (o.kind == 1) {
+				if (nrec >= rec_cap) st = 7;
+				else if (lane < 3) rec[3u * nrec + lane] = lane == 0 ? o.vs : (lane == 1 ? o.r_off : o.ve - o.vs);
+				++nrec;
+				dsz += 13;
+			} else {
+				dsz += 9ull + (o.ve - o.vs);
+			}
+			head = head + 1 == rcap ? 0 : head + 1;
+			--n;
+		}
+		if (vs < vl) dsz += 9ull + (vl - vs);
+	}
+	if (lane == 0) {
+		a.n_rec[pair] = nrec;
+		a.dsize[pair] = dsz;
+		a.status[pair] = st;
+	}
+}
+
+hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st) {
+	(void)p;
+	if (a.n_pairs == 0) return hipSuccess;
+	if (a.max_seeds) {
+		const dim3 grid(a.n_pairs, (a.max_seeds + kBuildSeedsPerBlock - 1) / kBuildSeedsPerBlock);
+		hipLaunchKernelGGL(correcting_build_kernel, grid, dim3(kBuildBlock), 0, st, a);
+	}
+	const size_t lds = sizeof(RingEnt) * ((size_t)(a.buf_cap ? a.buf_cap : 1) + 1);
+	hipLaunchKernelGGL(correcting_scan_kernel, dim3(a.n_pairs), dim3(64), lds, st, a);
+	return hipGetLastError();
+}
+
+}  // namespace dg

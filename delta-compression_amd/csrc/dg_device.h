@@ -33,7 +33,7 @@ struct PairPlanDev {
 	// correcting only (correcting.c:116-136)
 	uint64_t f_size, f_magic;  // |F| and floor((2^64-1)/|F|)
 	uint64_t m, m_magic;       // checkpoint modulus and Barrett
-	uint64_t k;                // biased class (computed on device)
+	uint64_t tab_base;         // first entry of this pair's R index (correcting)
 };
 
 struct CrcSegDev {        // one wave's CRC segment
@@ -73,8 +73,9 @@ struct EncodeArgs {
 	uint32_t* table_locks;
 	uint32_t* table_tags;
 	// correcting
-	uint32_t buf_cap;
-	uint32_t* cand;            // correcting candidate scratch (per pair)
+	uint32_t buf_cap;          // lookback buffer entries (correcting.c:14-62)
+	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
+	uint32_t max_seeds;        // max over pairs of |R| - p + 1
 };
 
 struct SerArgs {

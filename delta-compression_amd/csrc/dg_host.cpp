@@ -290,11 +290,13 @@ struct dg_encode_plan {
 	uint64_t out_bound = 0;
 	uint64_t total_rec = 0;
 	uint64_t qmax = 0;
+	uint64_t ctab_entries = 0;   // correcting: sum of per-pair index sizes
+	uint64_t max_seeds = 0;
 	uint32_t n_tables = 0;
 	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
-	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_cand;
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
@@ -328,6 +330,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		return set_err(ctx, DG_ERR_UNSUPPORTED, "in-place encode is not supported by the batch path");
 	if (o.p == 0) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len must be >= 1");
 	if (o.p > 65536) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len above 65536 is not supported");
+	if (algo == DG_ALGO_CORRECTING && o.buf_cap > 4095)
+		return set_err(ctx, DG_ERR_UNSUPPORTED, "--buffer-size above 4095 is not supported (LDS lookback ring)");
 	if (n > 0 && !pairs) return DG_ERR_INVALID_ARG;
 
 	dg_encode_plan_t* P = new (std::nothrow) dg_encode_plan_t();
@@ -341,7 +345,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	hipSetDevice(ctx->device);
 
 	std::map<uint64_t, uint64_t> qcache;
-	uint64_t rec = 0, bound = 0;
+	uint64_t rec = 0, bound = 0, ctab = 0;
 	const uint64_t p = o.p;
 	for (uint32_t i = 0; i < n; ++i) {
 		const dg_pair_t& d = pairs[i];
@@ -370,6 +374,9 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			x.m = x.f_size <= x.q ? 1 : (x.f_size + x.q - 1) / x.q;
 			x.f_magic = UINT64_MAX / x.f_size;
 			x.m_magic = UINT64_MAX / x.m;
+			x.tab_base = ctab;
+			ctab += x.q;
+			P->max_seeds = std::max<uint64_t>(P->max_seeds, seeds);
 		}
 		if (x.q >= 0xFFFFFFFFull) {
 			delete P;
@@ -379,12 +386,24 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		x.rec_base = rec;
 		x.rec_cap = (uint32_t)(d.v_len / p + 1);
 		rec += x.rec_cap;
-		// delta <= 35 + |V| + (|V|/p) * max(0, 22 - p)   
-		bound += 35 + d.v_len + (d.v_len / p) * (p < 22 ? 22 - p : 0);
+		// onepass: every COPY covers >= p bytes, so
+		//   delta <= 35 + |V| + (|V|/p) * max(0, 22 - p);
+		// correcting: a tail-corrected COPY may be shorter than p, but there
+		// are at most |V|/p + 1 of them, each with at most one ADD header
+		if (algo == DG_ALGO_ONEPASS)
+			bound += 35 + d.v_len + (d.v_len / p) * (p < 22 ? 22 - p : 0);
+		else
+			bound += 57 + d.v_len + 22 * (d.v_len / p);
 		P->qmax = std::max<uint64_t>(P->qmax, x.q);
 	}
 	P->out_bound = bound;
 	P->total_rec = rec;
+	P->ctab_entries = ctab;
+	if (ctab * 4 > (64ull << 30)) {
+		delete P;
+		return set_err(ctx, DG_ERR_NOMEM, "correcting R indexes need %llu GiB (limit 64)",
+		               (unsigned long long)(ctab >> 28));
+	}
 
 	// constants 263^(p-1-k) mod (2^61-1)
 	std::vector<uint64_t> powc(p);
@@ -430,6 +449,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_tables.alloc(per * P->n_tables);
 	bad |= P->d_locks.alloc(4ull * P->n_tables);
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
+	if (algo == DG_ALGO_CORRECTING) bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
 	if (bad) {
 		delete P;
 		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
@@ -577,11 +597,16 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.n_tables = P->n_tables;
 		a.table_locks = P->d_locks.as<uint32_t>();
 		a.table_tags = P->d_tags.as<uint32_t>();
-		a.buf_cap = (uint32_t)std::min<size_t>(P->opts.buf_cap, 1u << 20);
-		if (P->algo == DG_ALGO_ONEPASS)
+		a.buf_cap = (uint32_t)P->opts.buf_cap;
+		if (P->algo == DG_ALGO_ONEPASS) {
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
-		else
+		} else {
+			// fresh R indexes (~0 = empty slot), then build + scan
+			a.ctab = P->d_ctab.as<uint32_t>();
+			a.max_seeds = (uint32_t)P->max_seeds;
+			HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
 			HIPCHK(ctx, launch_correcting(a, a.p, st));
+		}
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[3], st));
 		return DG_OK;
 	};

@@ -610,6 +610,5 @@ hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* 
 	return hipGetLastError();
 }
 
-hipError_t launch_correcting(const EncodeArgs&, uint32_t, hipStream_t) { return hipErrorNotSupported; }
 
 }  // namespace dg

@@ -54,6 +54,26 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
+// ───────────────────────────── profiling build ────────────────────────────
+// make -C delta-compression_amd prof  →  lib/libdeltagpu_prof.so with per-wave
+// phase counters / cycle totals (scripts/onepass_phases.py).  Compiled out of
+// the product library.
+#ifdef DG_ONEPASS_PROF
+enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATCH, P_B_ENTRIES,
+       P_B_CHUNKS, P_C_CHUNKS, P_EXTENDS, P_REFILLS, P_T_DIAG, P_T_A, P_T_BC, P_T_EXT, P_T_REFILL,
+       P_T_TOTAL, P_B_WALKED, kProfN };
+__device__ unsigned long long g_onepass_prof[kProfN];
+#define PROF_DECL uint64_t prof[kProfN];
+#define PROF_INIT(o) for (int _i = 0; _i < kProfN; ++_i) (o).prof[_i] = 0;
+#define PROF_NOW() ((uint64_t)clock64())
+#define PROF_ADD(o, i, v) ((o).prof[(i)] += (uint64_t)(v))
+#else
+#define PROF_DECL
+#define PROF_INIT(o)
+#define PROF_NOW() 0ull
+#define PROF_ADD(o, i, v) ((void)0)
+#endif
+
 // ───────────────────────────── small helpers ──────────────────────────────
 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -133,6 +153,7 @@ struct WinSrc {
 	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
 	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
 	const uint64_t* powc;
+	PROF_DECL
 
 	// (re)load whichever window does not cover [lo, lo+need); both streams'
 	// LDS-DMA requests are in flight before the single wait
@@ -140,6 +161,7 @@ struct WinSrc {
 		const bool fv = wantV && (vlo < base[0] || vlo + need > base[0] + kWin);
 		const bool fr = wantR && (rlo < base[1] || rlo + need > base[1] + kWin);
 		if (!fv && !fr) return;
+		[[maybe_unused]] const uint64_t t0 = PROF_NOW();
 		const uint32_t lane = lane_id();
 		__syncthreads();   // the wave's reads of the old window are complete
 		// lane l's 16 bytes land at lds + 16*l (lane-linear).  Blocks past the
@@ -170,6 +192,8 @@ struct WinSrc {
 		}
 		vm_drain();        // the DMA landed (ordered by vmcnt) ...
 		__syncthreads();   // ... and is visible to every lane
+		PROF_ADD(*this, P_REFILLS, 1);
+		PROF_ADD(*this, P_T_REFILL, PROF_NOW() - t0);
 	}
 
 	// 4 bytes of stream s at offset x (little-endian), x inside the window
@@ -295,6 +319,8 @@ struct WinSrc {
 
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
 	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
+		[[maybe_unused]] const uint64_t t0 = PROF_NOW();
+		PROF_ADD(*this, P_EXTENDS, 1);
 		const uint32_t lane = lane_id();
 		uint32_t ml = 0;
 		while (ml < lim) {
@@ -306,10 +332,12 @@ struct WinSrc {
 			const uint64_t m = __ballot(fb < 4);
 			if (m) {
 				const uint32_t f = ffs64(m);
+				PROF_ADD(*this, P_T_EXT, PROF_NOW() - t0);
 				return ml + 4 * f + rdlane(fb, f);
 			}
 			ml += 256;
 		}
+		PROF_ADD(*this, P_T_EXT, PROF_NOW() - t0);
 		return lim;
 	}
 };
@@ -345,8 +373,13 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 		if constexpr (Src::kPhaseA) {
 			if (at_mismatch) {
 				uint32_t adv = 0, npred = 0;
+				[[maybe_unused]] const uint64_t td = PROF_NOW();
 				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, rec, nrec, rec_cap, bm,
 				                                      &adv, &npred));
+				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
+				PROF_ADD(src, P_DIAG_CALLS, 1);
+				PROF_ADD(src, P_DIAG_EPOCHS, f);
+				PROF_ADD(src, P_DIAG_ZERO, f == 0);
 				if (f) {
 					adv = uni(adv);
 					nrec += f;
@@ -367,6 +400,8 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 
 		// ── phase A: steps 0..7, four lanes per window ──
 		if constexpr (Src::kPhaseA) {
+			[[maybe_unused]] const uint64_t ta = PROF_NOW();
+			PROF_ADD(src, P_A_ENTRIES, 1);
 			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
 			const uint32_t side = lane >> 5, w = (lane >> 2) & 7u, part = lane & 3u;
 			const uint32_t bytes = src.rd4(side, (side ? r0 : v0) + w + 4 * part);
@@ -408,12 +443,16 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 					}
 				}
 			}
+			PROF_ADD(src, P_T_A, PROF_NOW() - ta);
+			PROF_ADD(src, P_A_MATCH, matched);
 			if (!matched && nlive <= 8) break;   // both streams exhausted: scan over
 		}
 
 		// ── phases B and C: 64 steps per chunk ──
 		uint32_t hsV[kHistChunks], hsR[kHistChunks], hfV[kHistChunks], hfR[kHistChunks];
 		bool in_table = false;
+		[[maybe_unused]] const uint64_t tb = PROF_NOW();
+		if constexpr (Src::kPhaseA) { if (!matched) PROF_ADD(src, P_B_ENTRIES, 1); }
 		for (uint32_t c = 0; !matched; ++c) {
 			const uint32_t b0 = 64 * c;
 			if (b0 >= nlive) { scanning = false; break; }   // both streams exhausted
@@ -427,6 +466,7 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 			if (cr) { fR = src.fpR(r0 + step); sR = (uint32_t)mod_q(fR, q, qmag); }
 			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
 
+			if constexpr (Src::kPhaseA) PROF_ADD(src, c < (uint32_t)kHistChunks ? P_B_CHUNKS : P_C_CHUNKS, 1);
 			if (c < (uint32_t)kHistChunks) {
 #pragma unroll
 				for (int k = 0; k < kHistChunks; ++k)
@@ -448,6 +488,7 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 				// steps phase A already ruled out are skipped
 				const uint32_t j0 = (Src::kPhaseA && c == 0) ? 8u : 0u;
 				uint64_t walk = (m1 | m2) & ~((1ull << j0) - 1ull);
+				if constexpr (Src::kPhaseA) PROF_ADD(src, P_B_WALKED, __builtin_popcountll(walk));
 				while (walk) {
 					const uint32_t j = ffs64(walk);
 					walk &= walk - 1;
@@ -545,6 +586,7 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 				}
 			}
 		}
+		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_BC, PROF_NOW() - tb);
 		if (!matched) break;
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
@@ -568,6 +610,13 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 		a.dsize[pair] = dsz;
 		a.status[pair] = st;
 	}
+#ifdef DG_ONEPASS_PROF
+	if constexpr (Src::kPhaseA) {
+		PROF_ADD(src, P_EPOCHS, nrec);
+		if (lane == 0)
+			for (int i = 0; i < kProfN; ++i) atomicAdd(&g_onepass_prof[i], (unsigned long long)src.prof[i]);
+	}
+#endif
 }
 
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
@@ -586,11 +635,16 @@ __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
 	src.win = (lds_u8*)win;
 	src.powc = a.powc;
+	PROF_INIT(src)
+	[[maybe_unused]] const uint64_t t_start = PROF_NOW();
 	uint64_t cA[4];
 	const uint32_t part = lane_id() & 3u;
 #pragma unroll
 	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
 	onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+#ifdef DG_ONEPASS_PROF
+	if (lane_id() == 0) atomicAdd(&g_onepass_prof[P_T_TOTAL], (unsigned long long)(PROF_NOW() - t_start));
+#endif
 }
 
 // any seed length or alignment, bytes from HBM/L2
@@ -622,5 +676,17 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 		hipLaunchKernelGGL(onepass_kernel<0>, dim3(a.n_pairs), dim3(64), 0, st, a);
 	return hipGetLastError();
 }
+
+#ifdef DG_ONEPASS_PROF
+extern "C" int dg_onepass_prof_read(unsigned long long* out, int n) {
+	if (n > kProfN) n = kProfN;
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_onepass_prof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+	return n;
+}
+extern "C" int dg_onepass_prof_reset(void) {
+	unsigned long long z[kProfN] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_onepass_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace dg

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-phase breakdown of onepass16_kernel (profiling build, DG_LIB_VARIANT=prof).
+
+usage: DG_LIB_VARIANT=prof python scripts/onepass_phases.py [--config c2] [--pairs N]
+Prints per-pair averages of the kernel's phase counters and cycle totals.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = ["epochs", "diag_calls", "diag_epochs", "diag_zero", "a_entries", "a_match", "b_entries",
+         "b_chunks", "c_chunks", "extends", "refills", "t_diag", "t_a", "t_bc", "t_ext", "t_refill",
+         "t_total", "b_walked"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--pairs", type=int, default=0)
+    args = ap.parse_args()
+    os.environ.setdefault("DG_LIB_VARIANT", "prof")
+    import torch
+    from bench import CONFIGS, load_product
+    dg = load_product()
+    L_ = dg.lib
+    L_.dg_onepass_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    L_.dg_onepass_prof_reset.argtypes = []
+    ctx = dg.Context(0)
+    npg, L, rate, q, seed, _ = CONFIGS[args.config]
+    n = args.pairs or npg
+    ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ctx.check(L_.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L, seed,
+                                            int(rate * L + 0.5), None), "synth")
+    plan = dg.EncodePlan(ctx, "onepass", [(i * L, L, i * L, L) for i in range(n)], q=q)
+    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr())
+    torch.cuda.synchronize()
+    L_.dg_onepass_prof_reset()
+    plan.set_timing(1)
+    plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr())
+    torch.cuda.synchronize()
+    buf = (C.c_ulonglong * len(NAMES))()
+    k = L_.dg_onepass_prof_read(buf, len(NAMES))
+    vals = {NAMES[i]: buf[i] / n for i in range(k)}
+    vals["stage_ms"] = plan.stage_times()
+    vals["pairs"] = n
+    print(json.dumps({k2: (round(v, 2) if isinstance(v, float) else v) for k2, v in vals.items()}))
+
+
+if __name__ == "__main__":
+    main()
