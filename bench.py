@@ -31,12 +31,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.join(ROOT, "delta-compression_amd")
 
 CONFIGS = {
-    # name: (pairs per GPU, pair bytes, edit rate, --table-size, seed base, description)
+    # name: (pairs per GPU, pair bytes, edit rate (< 0: transpositions, -pct), --table-size,
+    #        seed base, description, algorithm)
     "c2": (4096, 65536, 0.01, 1, 0xC2000000,
-           "4096 x 64 KiB pairs per GPU, 1% edits, onepass, --table-size 1"),
+           "4096 x 64 KiB pairs per GPU, 1% edits, onepass, --table-size 1", "onepass"),
     "c3": (8192, 262144, 0.10, 1, 0xC3000000,
-           "8192 x 256 KiB pairs per GPU (65536 on 8 GPUs), 10% edits, onepass, --table-size 1"),
+           "8192 x 256 KiB pairs per GPU (65536 on 8 GPUs), 10% edits, onepass, --table-size 1",
+           "onepass"),
+    "c4": (4096, 262144, -50, 1, 0xC4000000,
+           "4096 pairs of ~256 KiB per GPU, 8-64 block transpositions (50% moved), correcting, "
+           "--table-size 1", "correcting"),
 }
+ALGO_ID = {"onepass": 1, "correcting": 2}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -55,11 +61,12 @@ def cpu_baseline(cfg, n_pairs_sample, threads):
     """The reference's src/c (oracle/_ref/ref_bench, compiled from
     /root/reference by oracle/Makefile) on the host cores, bounded sample of
     the same workload.  Falls back to nothing if the build is absent."""
-    npg, L, rate, q, seed, _ = cfg
+    npg, L, rate, q, seed, _, algo = cfg
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     if not os.path.exists(exe):
         return None
-    cmd = [exe, "1", str(n_pairs_sample), str(L), str(rate), str(seed), str(threads), str(q), "3"]
+    cmd = [exe, str(ALGO_ID[algo]), str(n_pairs_sample), str(L), str(rate), str(seed), str(threads),
+           str(q), "3"]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
         res = json.loads(r.stdout.strip().splitlines()[-1])
@@ -71,7 +78,7 @@ def cpu_baseline(cfg, n_pairs_sample, threads):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "reference",
-        "sample": (f"{n_pairs_sample} pairs x {L} B of the same workload, src/c onepass "
+        "sample": (f"{n_pairs_sample} pairs x ~{L} B of the same workload, src/c {algo} "
                    f"(crc x2 + diff + place + encode), {threads} threads, best of 3"),
     }
 
@@ -84,7 +91,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pairs", type=int, default=2048)
+    ap.add_argument("--cpu-pairs", type=int, default=0,
+                    help="CPU baseline sample size (default: ~10-30 s of src/c work)")
     args = ap.parse_args()
 
     import torch
@@ -99,11 +107,10 @@ def main():
 
     dg = load_product()
     ctx = dg.Context(local)
-    npg, L, rate, q, seed_base, desc = CONFIGS[args.config]
+    npg, L, rate, q, seed_base, desc, algo = CONFIGS[args.config]
     if args.pairs:
         npg = args.pairs
-    cfg = (npg, L, rate, q, seed_base, desc)
-    n_edits = int(rate * L + 0.5)
+    cfg = (npg, L, rate, q, seed_base, desc, algo)
 
     # rank 0 decides the pair-index ranges and scatters them (RCCL broadcast)
     ranges = torch.tensor([[r * npg, (r + 1) * npg] for r in range(world)], dtype=torch.int64,
@@ -114,13 +121,29 @@ def main():
     n = hi - lo
 
     stream = torch.cuda.Stream()
-    ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L,
-                                                seed_base + lo, n_edits, stream.cuda_stream),
-              "synth")
-    plan = dg.EncodePlan(ctx, "onepass", [(i * L, L, i * L, L) for i in range(n)], q=q)
-    plan_aligned16 = (L % 16) == 0   # pairs packed at multiples of L
+    if rate >= 0:   # substitution pairs (C2/C3)
+        n_edits = int(rate * L + 0.5)
+        ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L,
+                                                    seed_base + lo, n_edits, stream.cuda_stream),
+                  "synth")
+        layout = [(i * L, L, i * L, L) for i in range(n)]
+    else:           # transposition pairs (C4)
+        import ctypes as C
+        pairs = (dg._lib.Pair * n)()
+        rb, vb = C.c_uint64(), C.c_uint64()
+        ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate),
+                                                         pairs, C.byref(rb), C.byref(vb), None, None,
+                                                         None), "layout")
+        ref = torch.empty(rb.value, dtype=torch.uint8, device="cuda")
+        ver = torch.empty(vb.value, dtype=torch.uint8, device="cuda")
+        ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate),
+                                                         pairs, C.byref(rb), C.byref(vb), ref.data_ptr(),
+                                                         ver.data_ptr(), stream.cuda_stream), "synth")
+        layout = [(x.r_off, x.r_len, x.v_off, x.v_len) for x in pairs]
+    plan = dg.EncodePlan(ctx, algo, layout, q=q)
+    plan_aligned16 = all((r_off | v_off) % 16 == 0 for r_off, _, v_off, _ in layout)
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -164,7 +187,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    in_bytes_rank = 2 * n * L
+    in_bytes_rank = sum(rl + vl for _, rl, _, vl in layout)
     total_bytes = in_bytes_rank * world * args.steps
     value = total_bytes / elapsed / 2**30
     avg_diff_s = diff_ms / args.steps / 1e3
@@ -184,13 +207,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)",
+            "data": ("synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)"
+                     if rate >= 0 else
+                     "synthetic (splitmix64 R, gen_transpositions.py-style block permutation, "
+                     "generated on device)"),
             "config": {
                 "workload": desc,
-                "algorithm": "onepass",
+                "algorithm": algo,
                 "pairs_per_gpu": n,
                 "pair_bytes": L,
-                "edit_rate": rate,
+                "edit_rate": rate if rate >= 0 else None,
+                "moved_block_pct": -rate if rate < 0 else None,
                 "table_size_floor": q,
                 "q": plan.table_size(0),
                 "seed_len": 16,
@@ -199,7 +226,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "onepass16_kernel" if plan_aligned16 else "onepass_kernel",
+                "kernel": ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
+                           else "onepass16_kernel" if plan_aligned16 else "onepass_kernel"),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -214,7 +242,9 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_pairs, threads)
+            # bounded sample: about 10-30 s of src/c work on `threads` cores
+            sample = args.cpu_pairs or {"c2": 2048, "c3": 256, "c4": 1024}[args.config]
+            line["cpu_baseline"] = cpu_baseline(cfg, sample, threads)
         print(json.dumps(line), flush=True)
 
     if world > 1:

@@ -128,6 +128,8 @@ def _load() -> C.CDLL:
         "dg_decode_batch_device": (C.c_int, [vp, vp, vp, C.POINTER(DecodeDesc), u32, C.c_int, vp, vp, vp, vp]),
         "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
         "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
+        "dg_synth_transpose_pairs_device": (C.c_int, [vp, u64, u32, u64, u32, C.POINTER(Pair),
+                                                      C.POINTER(u64), C.POINTER(u64), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -123,6 +123,13 @@ struct DecodeArgs {
 	const uint64_t* ref_crc;   // CRC-64/XZ of each reference span
 };
 
+struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off
+	uint64_t off, len, seed;
+};
+struct SynthCopy {   // V[dst..+len) = R[src..+len)
+	uint64_t dst, src, len;
+};
+
 // launchers (dg_kernels.hip)
 #ifdef __HIP_PLATFORM_AMD__
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
@@ -135,6 +142,8 @@ hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* 
                                 const uint64_t* out_crc, int32_t* status, hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);
+hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,
+                                  const SynthCopy* cmds, uint32_t n_cmds, hipStream_t st);
 #endif
 
 }  // namespace dg

@@ -191,6 +191,86 @@ int dg_synth_edit_pairs_device(dg_context_t* ctx, uint8_t* d_ref, uint8_t* d_ver
 	           : DG_ERR_HIP;
 }
 
+namespace {
+
+uint64_t splitmix_at_host(uint64_t seed, uint64_t k) {
+	uint64_t z = seed + k * 0x9E3779B97F4A7C15ULL;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+	return z ^ (z >> 31);
+}
+
+// One pair's block layout: sizes U[mean/2, 3 mean/2] (gen_transpositions.py
+// _gen_sizes), then a permutation moving round(nb * pct / 100) blocks
+// (_gen_perm: choose k distinct slots, shuffle their contents).
+void transpose_layout(uint64_t seed, uint32_t nb, uint32_t mean, uint32_t pct,
+                      std::vector<uint32_t>& sz, std::vector<uint32_t>& perm) {
+	const uint64_t s = seed ^ 0x5851F42D4C957F2DULL;
+	uint64_t k = 1;
+	const uint32_t lo = mean / 2 ? mean / 2 : 1, hi = mean * 3 / 2;
+	sz.resize(nb);
+	for (uint32_t i = 0; i < nb; ++i) sz[i] = lo + (uint32_t)(splitmix_at_host(s, k++) % (hi - lo + 1));
+	perm.resize(nb);
+	std::vector<uint32_t> idx(nb), val(nb);
+	for (uint32_t i = 0; i < nb; ++i) perm[i] = idx[i] = i;
+	const uint32_t kk = (uint32_t)(((uint64_t)nb * pct + 50) / 100);
+	if (kk < 2) return;
+	for (uint32_t j = 0; j < kk; ++j) {
+		const uint32_t t = j + (uint32_t)(splitmix_at_host(s, k++) % (nb - j));
+		std::swap(idx[j], idx[t]);
+	}
+	for (uint32_t j = 0; j < kk; ++j) val[j] = idx[j];
+	for (uint32_t j = kk - 1; j > 0; --j) {
+		const uint32_t t = (uint32_t)(splitmix_at_host(s, k++) % (j + 1));
+		std::swap(val[j], val[t]);
+	}
+	for (uint32_t j = 0; j < kk; ++j) perm[idx[j]] = val[j];
+}
+
+}  // namespace
+
+int dg_synth_transpose_pairs_device(dg_context_t* ctx, uint64_t seed_base, uint32_t n,
+                                    uint64_t target_len, uint32_t pct, dg_pair_t* pairs,
+                                    uint64_t* ref_bytes, uint64_t* ver_bytes, uint8_t* d_ref,
+                                    uint8_t* d_ver, void* stream) {
+	if (!ctx || (n && !pairs) || pct > 100 || target_len < 8) return DG_ERR_INVALID_ARG;
+	std::vector<dg::SynthSpan> spans(n);
+	std::vector<dg::SynthCopy> cmds;
+	std::vector<uint32_t> sz, perm, off;
+	uint64_t rt = 0, vt = 0;
+	for (uint32_t i = 0; i < n; ++i) {
+		const uint32_t nb = 8 + (i % 57);
+		transpose_layout(seed_base + i, nb, (uint32_t)(target_len / nb), pct, sz, perm);
+		off.assign(nb + 1, 0);
+		for (uint32_t b = 0; b < nb; ++b) off[b + 1] = off[b] + sz[b];
+		const uint64_t total = off[nb];
+		pairs[i] = dg_pair_t{rt, total, vt, total};
+		spans[i] = dg::SynthSpan{rt, total, seed_base + i};
+		uint64_t o = 0;
+		for (uint32_t b = 0; b < nb; ++b) {
+			cmds.push_back(dg::SynthCopy{vt + o, rt + off[perm[b]], sz[perm[b]]});
+			o += sz[perm[b]];
+		}
+		rt += up16(total);
+		vt += up16(total);
+	}
+	if (ref_bytes) *ref_bytes = rt;
+	if (ver_bytes) *ver_bytes = vt;
+	if (!d_ref) return DG_OK;
+	if (!d_ver) return DG_ERR_INVALID_ARG;
+	hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)dg_context_stream(ctx);
+	Dev d_spans, d_cmds;
+	if (!d_spans.alloc(sizeof(dg::SynthSpan) * n) || !d_cmds.alloc(sizeof(dg::SynthCopy) * cmds.size()))
+		return DG_ERR_NOMEM;
+	if (hipMemcpyAsync(d_spans.p, spans.data(), sizeof(dg::SynthSpan) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+	    hipMemcpyAsync(d_cmds.p, cmds.data(), sizeof(dg::SynthCopy) * cmds.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+	    dg::launch_synth_transpose(d_ref, d_ver, d_spans.as<dg::SynthSpan>(), n, d_cmds.as<dg::SynthCopy>(),
+	                               (uint32_t)cmds.size(), st) != hipSuccess ||
+	    hipStreamSynchronize(st) != hipSuccess)
+		return DG_ERR_HIP;
+	return DG_OK;
+}
+
 }  // extern "C"
 
 // ───────────────────────────── decode ─────────────────────────────────────

@@ -344,11 +344,40 @@ __global__ __launch_bounds__(64) void synth_edits_kernel(uint8_t* ver, uint32_t 
 	}
 }
 
+// Transposition pairs (tests/gen_transpositions.py recipe, planned on the
+// host): R bytes are the splitmix64 stream of the pair's seed; V is R's
+// blocks in permuted order, one copy command per block.
+__global__ __launch_bounds__(256) void synth_stream_kernel(uint8_t* ref, const SynthSpan* spans,
+                                                           uint32_t n) {
+	const uint32_t i = blockIdx.y;
+	if (i >= n) return;
+	const SynthSpan sp = spans[i];
+	const uint64_t words = (sp.len + 7) / 8;
+	for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < words; k += (uint64_t)gridDim.x * 256) {
+		const uint64_t val = splitmix_at(sp.seed, k + 1);
+		uint8_t* r = ref + sp.off + 8 * k;
+		for (uint64_t b = 0; b < 8 && 8 * k + b < sp.len; ++b) r[b] = (uint8_t)(val >> (8 * b));
+	}
+}
+
+__global__ __launch_bounds__(256) void synth_copy_kernel(uint8_t* ver, const uint8_t* ref,
+                                                         const SynthCopy* cmds, uint32_t n) {
+	const SynthCopy c = cmds[blockIdx.x];
+	for (uint64_t b = threadIdx.x; b < c.len; b += 256) ver[c.dst + b] = ref[c.src + b];
+}
+
 }  // namespace dg
 
 // ───────────────────────────── launchers (C++ linkage, internal) ──────────
 
 namespace dg {
+
+hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,
+                                  const SynthCopy* cmds, uint32_t n_cmds, hipStream_t st) {
+	if (n_spans) hipLaunchKernelGGL(synth_stream_kernel, dim3(64, n_spans), dim3(256), 0, st, ref, spans, n_spans);
+	if (n_cmds) hipLaunchKernelGGL(synth_copy_kernel, dim3(n_cmds), dim3(256), 0, st, ver, ref, cmds, n_cmds);
+	return hipGetLastError();
+}
 
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);

@@ -255,6 +255,18 @@ int dg_synth_edit_pairs_device(dg_context_t *ctx, uint8_t *d_ref,
                                uint8_t *d_ver, uint32_t n_pairs,
                                uint64_t pair_len, uint64_t seed_base,
                                uint64_t n_edits, void *stream);
+/* C4 transposition pairs (tests/gen_transpositions.py _gen_sizes/_gen_perm
+ * with a per-pair splitmix64 seed seed_base + i): pair i has
+ * num_blocks = 8 + (i mod 57) blocks of mean size target_len / num_blocks,
+ * pct % of them permuted.  Pairs are packed at 16-byte aligned offsets,
+ * written to pairs[n].  With d_ref == NULL only the layout is computed and
+ * *ref_bytes / *ver_bytes receive the arena sizes to allocate. */
+int dg_synth_transpose_pairs_device(dg_context_t *ctx, uint64_t seed_base,
+                                    uint32_t n_pairs, uint64_t target_len,
+                                    uint32_t pct, dg_pair_t *pairs,
+                                    uint64_t *ref_bytes, uint64_t *ver_bytes,
+                                    uint8_t *d_ref, uint8_t *d_ver,
+                                    void *stream);
 
 #ifdef __cplusplus
 }

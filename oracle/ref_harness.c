@@ -81,6 +81,7 @@ typedef struct {
 	int algo;
 	size_t n_pairs, len, p, q;
 	uint8_t **r, **v;
+	size_t *lens;           /* per pair |R| = |V| */
 	size_t next;
 	pthread_mutex_t mu;
 	unsigned long long out_bytes;
@@ -96,7 +97,7 @@ static void *worker(void *arg)
 		pthread_mutex_unlock(&j->mu);
 		if (i >= j->n_pairs) break;
 		uint8_t *d = NULL;
-		ob += ref_encode_pair(j->algo, j->r[i], j->len, j->v[i], j->len,
+		ob += ref_encode_pair(j->algo, j->r[i], j->lens[i], j->v[i], j->lens[i],
 		                      j->p, j->q, DELTA_BUF_CAP,
 		                      DELTA_MAX_TABLE_SIZE, &d);
 		free(d);
@@ -114,7 +115,9 @@ static double now(void)
 	return t.tv_sec + t.tv_nsec / 1e9;
 }
 
-/* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps */
+/* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps
+ * edit_rate >= 0: C2/C3 substitution pairs; edit_rate < 0: C4 transposition
+ * pairs (num_blocks = 8 + i mod 57, -edit_rate percent of blocks moved). */
 int main(int argc, char **argv)
 {
 	if (argc < 9) {
@@ -134,13 +137,25 @@ int main(int argc, char **argv)
 	j.p = DELTA_SEED_LEN;
 	j.r = malloc(j.n_pairs * sizeof(uint8_t *));
 	j.v = malloc(j.n_pairs * sizeof(uint8_t *));
-	unsigned long long n_edits = (unsigned long long)(rate * (double)j.len + 0.5);
+	j.lens = malloc(j.n_pairs * sizeof(size_t));
+	unsigned long long n_edits = rate > 0 ? (unsigned long long)(rate * (double)j.len + 0.5) : 0;
+	double total_in = 0;
 	for (size_t i = 0; i < j.n_pairs; i++) {
-		j.r[i] = malloc(j.len);
-		j.v[i] = malloc(j.len);
-		or_synth_random(seed + i, j.r[i], j.len);
-		memcpy(j.v[i], j.r[i], j.len);
-		or_synth_edits(seed + i, j.v[i], j.len, n_edits);
+		if (rate < 0) {
+			uint32_t nb = 8 + (uint32_t)(i % 57), mean = (uint32_t)(j.len / nb);
+			size_t cap = (size_t)nb * (mean * 3 / 2 + 1);
+			j.r[i] = malloc(cap);
+			j.v[i] = malloc(cap);
+			j.lens[i] = or_synth_transpose(seed + i, nb, mean, (uint32_t)(-rate), j.r[i], j.v[i], cap);
+		} else {
+			j.r[i] = malloc(j.len);
+			j.v[i] = malloc(j.len);
+			j.lens[i] = j.len;
+			or_synth_random(seed + i, j.r[i], j.len);
+			memcpy(j.v[i], j.r[i], j.len);
+			or_synth_edits(seed + i, j.v[i], j.len, n_edits);
+		}
+		total_in += 2.0 * (double)j.lens[i];
 	}
 	{   /* warm the reference's lazy CRC table before threads start */
 		uint8_t c[8];
@@ -162,7 +177,7 @@ int main(int argc, char **argv)
 		sum += dt;
 		out_bytes = j.out_bytes;
 	}
-	double in_bytes = 2.0 * (double)j.len * (double)j.n_pairs;
+	double in_bytes = total_in;
 	printf("{\"pairs\": %zu, \"pair_len\": %zu, \"threads\": %d, \"reps\": %d, "
 	       "\"best_s\": %.6f, \"mean_s\": %.6f, \"in_bytes\": %.0f, "
 	       "\"out_bytes\": %llu, \"gib_per_s\": %.6f}\n",

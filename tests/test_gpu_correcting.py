@@ -105,3 +105,40 @@ def test_correcting_low_entropy(dg, ctx, orc, buf_cap):
                               buf_cap=buf_cap, ctx=ctx)
         for (name, R, V), g in zip(items, got):
             assert g == orc.encode(CORRECTING, R, V, p=p, q=q, buf_cap=buf_cap), (name, buf_cap)
+
+
+def test_correcting_c4_device_batch(dg, ctx, orc, torch_cuda):
+    """C4 batch generated on the device (dg_synth_transpose_pairs_device) equals
+    the oracle's generator; encoded through the plan API, sampled pairs are
+    bit-exact and the rest are checked by status."""
+    import ctypes as C
+    torch = torch_cuda
+    n, target, seed = 128, 262144, 0xC4000000
+    pairs = (dg._lib.Pair * n)()
+    rb, vb = C.c_uint64(), C.c_uint64()
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), None, None, None), "layout")
+    ref = torch.empty(rb.value, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(vb.value, dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), ref.data_ptr(),
+                                                     ver.data_ptr(), None), "synth")
+    lay = [(p.r_off, p.r_len, p.v_off, p.v_len) for p in pairs]
+    plan = dg.EncodePlan(ctx, "correcting", lay, q=1)
+    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+    off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), off.data_ptr(),
+             st.data_ptr(), ctx.stream)
+    torch.cuda.synchronize()
+    assert int(st.abs().sum()) == 0
+    offs = off.cpu().tolist()
+    refc, verc, outc = ref.cpu(), ver.cpu(), out.cpu()
+    for i in list(range(0, n, 9)) + [n - 1]:
+        nb = 8 + (i % 57)
+        R, V = orc.synth_transpose(seed + i, nb, target // nb, 50)
+        ro, rl, vo, vl = lay[i]
+        assert bytes(refc[ro:ro + rl].numpy()) == R
+        assert bytes(verc[vo:vo + vl].numpy()) == V
+        assert bytes(outc[offs[i]:offs[i + 1]].numpy()) == orc.encode(CORRECTING, R, V, p=16, q=1), i
