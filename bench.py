@@ -41,8 +41,12 @@ CONFIGS = {
     "c4": (4096, 262144, -50, 1, 0xC4000000,
            "4096 pairs of ~256 KiB per GPU, 8-64 block transpositions (50% moved), correcting, "
            "--table-size 1", "correcting"),
+    # C5: decode + CRC-64/XZ verify of C2-style deltas (1024 streams, ~1.1M commands)
+    "c5": (1024, 65536, 0.01, 1, 0xC2000000,
+           "1024 onepass deltas of C2 pairs (~1.1M COPY/ADD commands), decode + src/dst CRC "
+           "verify on device", "decode"),
 }
-ALGO_ID = {"onepass": 1, "correcting": 2}
+ALGO_ID = {"onepass": 1, "correcting": 2, "decode": 11}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -78,9 +82,92 @@ def cpu_baseline(cfg, n_pairs_sample, threads):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "reference",
-        "sample": (f"{n_pairs_sample} pairs x ~{L} B of the same workload, src/c {algo} "
-                   f"(crc x2 + diff + place + encode), {threads} threads, best of 3"),
+        "sample": (f"{n_pairs_sample} pairs x ~{L} B of the same workload, src/c "
+                   + ("delta_decode + apply + src/dst CRC checks" if algo == "decode" else
+                      f"{algo} (crc x2 + diff + place + encode)")
+                   + f", {threads} threads, best of 3"),
     }
+
+
+def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, ver, stream, cfg):
+    """C5: the deltas of this rank's pairs are produced on the device first
+    (untimed); one step = dg_decode_plan_run over all of them (reference CRC
+    on a side stream, decode, output CRC, verify)."""
+    enc = dg.EncodePlan(ctx, "onepass", layout, q=q)
+    d_arena = torch.empty(enc.output_bound, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    est = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc.run(ref.data_ptr(), ver.data_ptr(), d_arena.data_ptr(), d_arena.numel(), offs.data_ptr(),
+            est.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    assert int(est.abs().sum()) == 0
+    o = offs.cpu().tolist()
+    descs = [(r_off, r_len, o[i], o[i + 1] - o[i], v_off, v_len)
+             for i, (r_off, r_len, v_off, v_len) in enumerate(layout)]
+    plan = dg.DecodePlan(ctx, descs)
+    out = torch.empty_like(ver)
+    out_len = torch.empty(n, dtype=torch.int64, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+
+    def step():
+        plan.run(ref.data_ptr(), d_arena.data_ptr(), out.data_ptr(), out_len.data_ptr(),
+                 status.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    out.zero_()
+    step()
+    torch.cuda.synchronize()
+    if int(status.abs().sum()) != 0 or not torch.equal(out, ver):
+        raise SystemExit(f"decode failed: status {status.unique().tolist()}")
+    plan.set_timing(args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = plan.stage_times()
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    v_bytes = sum(vl for _, _, _, vl in layout)
+    d_bytes = o[-1]
+    dec_ms = stages.get("decode", 0.0)
+    # decode_kernel algorithmic bytes: the deltas read, COPY sources read and
+    # the outputs written (<= |delta| + 2 sum|V|)
+    alg = d_bytes + 2 * v_bytes
+    achieved = alg / (dec_ms / 1e3) / 1e9 if dec_ms > 0 else 0.0
+    if rank == 0:
+        line = {
+            "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
+            "value": round(v_bytes * world * args.steps / elapsed / 2**30, 3),
+            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (C2 pairs generated on device, deltas from the device encoder)",
+            "config": {"workload": cfg[5], "streams_per_gpu": n, "delta_bytes_per_gpu": d_bytes,
+                       "parallelism": f"dp{world} (stream shards)"},
+            "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dec_ms, 4),
+                         "stage_ms": {k: round(v, 4) for k, v in stages.items()}},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_pairs or 4096, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -142,6 +229,9 @@ def main():
                                                          pairs, C.byref(rb), C.byref(vb), ref.data_ptr(),
                                                          ver.data_ptr(), stream.cuda_stream), "synth")
         layout = [(x.r_off, x.r_len, x.v_off, x.v_len) for x in pairs]
+    if algo == "decode":
+        return decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, ver, stream,
+                            cfg)
     plan = dg.EncodePlan(ctx, algo, layout, q=q)
     plan_aligned16 = all((r_off | v_off) % 16 == 0 for r_off, _, v_off, _ in layout)
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")

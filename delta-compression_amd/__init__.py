@@ -30,6 +30,7 @@ from ._lib import (  # noqa: F401
     DeltaError,
     DiffOptions,
     EncodePlan,
+    DecodePlan,
     LIB_PATH,
     crc64_xz,
     decode,
@@ -43,7 +44,7 @@ from ._lib import (  # noqa: F401
 
 __all__ = [
     "ALGO_ONEPASS", "ALGO_CORRECTING", "ALGO_GREEDY", "SEED_LEN", "TABLE_SIZE",
-    "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan",
+    "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan", "DecodePlan",
     "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
     "status_string", "LIB_PATH",
 ]

@@ -126,6 +126,11 @@ def _load() -> C.CDLL:
         "dg_crc64_xz_batch_device": (C.c_int, [vp, vp, C.POINTER(Span), u32, vp, vp]),
         "dg_decode": (C.c_int, [vp, u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer)]),
         "dg_decode_batch_device": (C.c_int, [vp, vp, vp, C.POINTER(DecodeDesc), u32, C.c_int, vp, vp, vp, vp]),
+        "dg_decode_plan_create": (C.c_int, [vp, C.POINTER(DecodeDesc), u32, C.c_int, C.POINTER(vp)]),
+        "dg_decode_plan_run": (C.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+        "dg_decode_plan_set_timing": (C.c_int, [vp, C.c_int]),
+        "dg_decode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
+        "dg_decode_plan_destroy": (None, [vp]),
         "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
         "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
         "dg_synth_transpose_pairs_device": (C.c_int, [vp, u64, u32, u64, u32, C.POINTER(Pair),
@@ -252,6 +257,46 @@ class EncodePlan:
     def close(self):
         if getattr(self, "handle", None):
             lib.dg_encode_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DecodePlan:
+    """dg_decode_plan_t: batched device decode + CRC verify (C5)."""
+
+    def __init__(self, ctx: Context, descs: Sequence[Tuple[int, int, int, int, int, int]],
+                 ignore_hash: bool = False):
+        self.ctx = ctx
+        n = len(descs)
+        arr = (DecodeDesc * max(n, 1))(*[DecodeDesc(*d) for d in descs])
+        h = C.c_void_p()
+        ctx.check(lib.dg_decode_plan_create(ctx.handle, arr, n, int(ignore_hash), C.byref(h)),
+                  "dg_decode_plan_create")
+        self.handle = h
+        self.n = n
+
+    def run(self, d_ref: int, d_delta: int, d_out: int, d_out_len: int, d_status: int,
+            stream: int = 0):
+        self.ctx.check(lib.dg_decode_plan_run(self.handle, d_ref, d_delta, d_out, d_out_len, d_status,
+                                              stream or None), "dg_decode_plan_run")
+
+    def set_timing(self, slots: int = 1):
+        self.ctx.check(lib.dg_decode_plan_set_timing(self.handle, int(slots)), "set_timing")
+
+    def stage_times(self):
+        ms = (C.c_float * 8)()
+        names = (C.c_char_p * 8)()
+        k = lib.dg_decode_plan_stage_times(self.handle, ms, names, 8)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def close(self):
+        if self.handle:
+            lib.dg_decode_plan_destroy(self.handle)
             self.handle = None
 
     def __del__(self):

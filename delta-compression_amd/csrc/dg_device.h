@@ -116,11 +116,10 @@ struct DecodeArgs {
 	const uint8_t* delta;
 	const dg_decode_desc_dev* descs;
 	uint32_t n;
-	int ignore_hash;
 	uint8_t* out;
 	uint64_t* out_len;
 	int32_t* status;
-	const uint64_t* ref_crc;   // CRC-64/XZ of each reference span
+	CrcSpanDev* out_spans;     // nullable: span i's length := version size (for the dst CRC)
 };
 
 struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off
@@ -139,7 +138,8 @@ hipError_t launch_serialize(const SerArgs& s, hipStream_t st);
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
-                                const uint64_t* out_crc, int32_t* status, hipStream_t st);
+                                const uint64_t* ref_crc, const uint64_t* out_crc, int32_t* status,
+                                hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);
 hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,

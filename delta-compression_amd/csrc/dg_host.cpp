@@ -698,3 +698,216 @@ extern "C" int dg_crc64_xz_batch_device(dg_context_t* ctx, const uint8_t* d_aren
 	HIPCHK(ctx, hipStreamSynchronize(st));   // the temporaries die here
 	return DG_OK;
 }
+
+// ───────────────────────────── decode plan ────────────────────────────────
+
+struct dg_decode_plan {
+	dg_context_t* ctx = nullptr;
+	uint32_t n = 0;
+	int ignore_hash = 0;
+	DevBuf d_desc;
+	// reference CRC (side stream) and output CRC (after decode)
+	DevBuf d_rspans, d_rsegs, d_rsegc, d_rcrc;
+	DevBuf d_ospans, d_osegs, d_osegc, d_ocrc;
+	uint32_t n_rsegs = 0, n_osegs = 0;
+	hipStream_t side = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	bool timing = false;
+	std::vector<hipEvent_t> ev;
+	uint32_t slots = 0, runs = 0;
+};
+
+namespace {
+constexpr int kDecEvents = 5;
+const char* kDecStageNames[] = {"ref_crc", "decode", "out_crc+verify", "total"};
+}  // namespace
+
+extern "C" {
+
+int dg_decode_plan_create(dg_context_t* ctx, const dg_decode_desc_t* descs, uint32_t n,
+                          int ignore_hash, dg_decode_plan_t** out) {
+	if (!ctx || !out || (n && !descs)) return DG_ERR_INVALID_ARG;
+	*out = nullptr;
+	hipSetDevice(ctx->device);
+	auto* P = new (std::nothrow) dg_decode_plan_t();
+	if (!P) return DG_ERR_NOMEM;
+	P->ctx = ctx;
+	P->n = n;
+	P->ignore_hash = ignore_hash;
+	for (uint32_t i = 0; i < n; ++i)
+		if (descs[i].ref_len >= (1ull << 32) || descs[i].out_cap >= (1ull << 32) + (1ull << 31)) {
+			delete P;
+			return set_err(ctx, DG_ERR_TOO_LARGE, "stream %u exceeds the u32 format", i);
+		}
+	std::vector<dg_span_t> rs(n), os(n);
+	std::vector<uint32_t> w0(n, 0), w1(n, 1);
+	for (uint32_t i = 0; i < n; ++i) {
+		rs[i] = dg_span_t{descs[i].ref_off, descs[i].ref_len};
+		os[i] = dg_span_t{descs[i].out_off, descs[i].out_cap};   // length patched on device
+	}
+	std::vector<CrcSpanDev> rsd, osd;
+	std::vector<CrcSegDev> rseg, oseg;
+	plan_crc_spans(rs, w0, rsd, rseg);
+	plan_crc_spans(os, w1, osd, oseg);
+	P->n_rsegs = (uint32_t)rseg.size();
+	P->n_osegs = (uint32_t)oseg.size();
+	const size_t nn = std::max<size_t>(n, 1);
+	int bad = 0;
+	bad |= P->d_desc.alloc(sizeof(dg_decode_desc_t) * nn);
+	bad |= P->d_rspans.alloc(sizeof(CrcSpanDev) * nn);
+	bad |= P->d_rsegs.alloc(sizeof(CrcSegDev) * std::max<size_t>(rseg.size(), 1));
+	bad |= P->d_rsegc.alloc(8 * std::max<size_t>(rseg.size(), 1));
+	bad |= P->d_rcrc.alloc(8 * nn);
+	bad |= P->d_ospans.alloc(sizeof(CrcSpanDev) * nn);
+	bad |= P->d_osegs.alloc(sizeof(CrcSegDev) * std::max<size_t>(oseg.size(), 1));
+	bad |= P->d_osegc.alloc(8 * std::max<size_t>(oseg.size(), 1));
+	bad |= P->d_ocrc.alloc(8 * nn);
+	if (bad) {
+		delete P;
+		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
+	}
+	hipStream_t st = ctx->stream;
+	hipError_t e = hipSuccess;
+	if (n) {
+		e = hipMemcpyAsync(P->d_desc.p, descs, sizeof(dg_decode_desc_t) * n, hipMemcpyHostToDevice, st);
+		if (e == hipSuccess) e = hipMemcpyAsync(P->d_rspans.p, rsd.data(), sizeof(CrcSpanDev) * n, hipMemcpyHostToDevice, st);
+		// output spans: segmentation sized for out_cap; every run's decoder
+		// rewrites each span's length from its delta header before the CRC
+		if (e == hipSuccess) e = hipMemcpyAsync(P->d_ospans.p, osd.data(), sizeof(CrcSpanDev) * n, hipMemcpyHostToDevice, st);
+		if (e == hipSuccess && !rseg.empty())
+			e = hipMemcpyAsync(P->d_rsegs.p, rseg.data(), sizeof(CrcSegDev) * rseg.size(), hipMemcpyHostToDevice, st);
+		if (e == hipSuccess && !oseg.empty())
+			e = hipMemcpyAsync(P->d_osegs.p, oseg.data(), sizeof(CrcSegDev) * oseg.size(), hipMemcpyHostToDevice, st);
+	}
+	if (e == hipSuccess) e = hipStreamSynchronize(st);
+	if (e == hipSuccess) e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
+	if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
+	if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_join, hipEventDisableTiming);
+	if (e != hipSuccess) {
+		dg_decode_plan_destroy(P);
+		return set_err(ctx, DG_ERR_HIP, "decode plan setup failed: %s", hipGetErrorString(e));
+	}
+	*out = P;
+	return DG_OK;
+}
+
+int dg_decode_plan_set_timing(dg_decode_plan_t* P, int slots) {
+	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
+	hipSetDevice(P->ctx->device);
+	if ((uint32_t)slots > P->slots) {
+		for (auto& e : P->ev) hipEventDestroy(e);
+		P->ev.assign((size_t)kDecEvents * slots, nullptr);
+		for (auto& e : P->ev)
+			if (hipEventCreate(&e) != hipSuccess) {
+				e = nullptr;
+				return set_err(P->ctx, DG_ERR_HIP, "hipEventCreate failed");
+			}
+		P->slots = (uint32_t)slots;
+	}
+	P->timing = slots > 0;
+	P->runs = 0;
+	return DG_OK;
+}
+
+// events: 0/1 around the reference CRC (side stream), 2 decode start,
+// 3 decode end, 4 after the output CRC + verify
+int dg_decode_plan_stage_times(dg_decode_plan_t* P, float* ms, const char** names, int n) {
+	if (!P || !P->slots || !P->runs) return 0;
+	const uint32_t used = std::min(P->runs, P->slots);
+	const int pairs[4][2] = {{0, 1}, {2, 3}, {3, 4}, {2, 4}};
+	double acc[4] = {};
+	for (uint32_t s = 0; s < used; ++s) {
+		hipEvent_t* e = &P->ev[(size_t)kDecEvents * s];
+		if (hipEventSynchronize(e[4]) != hipSuccess) return 0;
+		for (int k = 0; k < 4; ++k) {
+			float t = 0;
+			hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]);
+			acc[k] += t;
+		}
+	}
+	int k = 0;
+	for (; k < 4 && k < n; ++k) {
+		if (ms) ms[k] = (float)(acc[k] / used);
+		if (names) names[k] = kDecStageNames[k];
+	}
+	return k;
+}
+
+int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t* d_delta,
+                       uint8_t* d_out, uint64_t* d_out_len, int32_t* d_status, void* stream) {
+	if (!P) return DG_ERR_INVALID_ARG;
+	dg_context_t* ctx = P->ctx;
+	if (P->n == 0) return DG_OK;
+	if (!d_ref || !d_delta || !d_out || !d_out_len || !d_status)
+		return set_err(ctx, DG_ERR_INVALID_ARG, "null device buffer");
+	if (((uintptr_t)d_ref & 15) || ((uintptr_t)d_out & 15))
+		return set_err(ctx, DG_ERR_INVALID_ARG, "arena base pointers must be 16-byte aligned");
+	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+	hipEvent_t* ev = nullptr;
+	if (P->timing) ev = &P->ev[(size_t)kDecEvents * (P->runs++ % P->slots)];
+	auto crc_args = [&](const uint8_t* arena, DevBuf& spans, DevBuf& segs, uint32_t nsegs, DevBuf& segc,
+	                    DevBuf& outc) {
+		CrcArgs a{};
+		a.arena[0] = a.arena[1] = arena;
+		a.spans = spans.as<CrcSpanDev>();
+		a.segs = segs.as<CrcSegDev>();
+		a.n_segs = nsegs;
+		a.n_spans = P->n;
+		a.tables = ctx->d_crc_tables;
+		a.seg_crc = segc.as<uint64_t>();
+		a.out = outc.as<uint64_t>();
+		a.xinv = ctx->d_xinv;
+		a.kseg = ctx->kseg;
+		return a;
+	};
+	const bool check = !P->ignore_hash;
+	if (check) {   // 1. CRC of every reference span, forked (main.c:341-356)
+		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
+		HIPCHK(ctx, hipStreamWaitEvent(P->side, P->ev_fork, 0));
+		if (ev) HIPCHK(ctx, hipEventRecord(ev[0], P->side));
+		HIPCHK(ctx, launch_crc(crc_args(d_ref, P->d_rspans, P->d_rsegs, P->n_rsegs, P->d_rsegc, P->d_rcrc),
+		                       P->side));
+		if (ev) HIPCHK(ctx, hipEventRecord(ev[1], P->side));
+		HIPCHK(ctx, hipEventRecord(P->ev_join, P->side));
+	} else if (ev) {
+		HIPCHK(ctx, hipEventRecord(ev[0], st));
+		HIPCHK(ctx, hipEventRecord(ev[1], st));
+	}
+	// 2. parse + apply (encoding.c:111-178, apply.c:229-284)
+	if (ev) HIPCHK(ctx, hipEventRecord(ev[2], st));
+	DecodeArgs a{};
+	a.ref = d_ref;
+	a.delta = d_delta;
+	a.descs = P->d_desc.as<dg_decode_desc_dev>();
+	a.n = P->n;
+	a.out = d_out;
+	a.out_len = d_out_len;
+	a.status = d_status;
+	a.out_spans = check ? P->d_ospans.as<CrcSpanDev>() : nullptr;
+	HIPCHK(ctx, launch_decode(a, st));
+	if (ev) HIPCHK(ctx, hipEventRecord(ev[3], st));
+	// 3. CRC of every output, then the checks (main.c:376-385)
+	if (check) {
+		HIPCHK(ctx, launch_crc(crc_args(d_out, P->d_ospans, P->d_osegs, P->n_osegs, P->d_osegc, P->d_ocrc), st));
+		HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
+		HIPCHK(ctx, launch_decode_verify(d_delta, a.descs, P->n, P->d_rcrc.as<uint64_t>(),
+		                                 P->d_ocrc.as<uint64_t>(), d_status, st));
+	}
+	if (ev) HIPCHK(ctx, hipEventRecord(ev[4], st));
+	return DG_OK;
+}
+
+void dg_decode_plan_destroy(dg_decode_plan_t* P) {
+	if (!P) return;
+	hipSetDevice(P->ctx->device);
+	hipStreamSynchronize(P->ctx->stream);
+	if (P->side) hipStreamSynchronize(P->side);
+	for (auto& e : P->ev)
+		if (e) hipEventDestroy(e);
+	if (P->ev_fork) hipEventDestroy(P->ev_fork);
+	if (P->ev_join) hipEventDestroy(P->ev_join);
+	if (P->side) hipStreamDestroy(P->side);
+	delete P;
+}
+
+}  // extern "C"

@@ -279,49 +279,18 @@ extern "C" int dg_decode_batch_device(dg_context_t* ctx, const uint8_t* d_ref,
                                       const uint8_t* d_delta, const dg_decode_desc_t* descs,
                                       uint32_t n, int ignore_hash, uint8_t* d_out,
                                       uint64_t* d_out_len, int32_t* d_status, void* stream) {
+	// one-shot plan: create, run, wait, release
 	if (!ctx || (n && (!d_ref || !d_delta || !descs || !d_out || !d_out_len || !d_status)))
 		return DG_ERR_INVALID_ARG;
 	if (n == 0) return DG_OK;
-	if (((uintptr_t)d_ref & 15) || ((uintptr_t)d_out & 15)) return DG_ERR_INVALID_ARG;
+	dg_decode_plan_t* plan = nullptr;
+	int rc = dg_decode_plan_create(ctx, descs, n, ignore_hash, &plan);
+	if (rc) return rc;
 	hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)dg_context_stream(ctx);
-	Dev d_desc, d_rcrc, d_ocrc;
-	if (!d_desc.alloc(sizeof(dg_decode_desc_t) * n) || !d_rcrc.alloc(8ull * n) || !d_ocrc.alloc(8ull * n))
-		return DG_ERR_NOMEM;
-	if (hipMemcpyAsync(d_desc.p, descs, sizeof(dg_decode_desc_t) * n, hipMemcpyHostToDevice, st) != hipSuccess)
-		return DG_ERR_HIP;
-	// 1. CRC of every reference span (main.c:341-356)
-	if (!ignore_hash) {
-		std::vector<dg_span_t> sp(n);
-		for (uint32_t i = 0; i < n; ++i) sp[i] = dg_span_t{descs[i].ref_off, descs[i].ref_len};
-		int rc = dg_crc64_xz_batch_device(ctx, d_ref, sp.data(), n, d_rcrc.as<uint64_t>(), st);
-		if (rc) return rc;
-	}
-	// 2. parse + apply
-	dg::DecodeArgs a{};
-	a.ref = d_ref;
-	a.delta = d_delta;
-	a.descs = d_desc.as<dg::dg_decode_desc_dev>();
-	a.n = n;
-	a.ignore_hash = ignore_hash;
-	a.out = d_out;
-	a.out_len = d_out_len;
-	a.status = d_status;
-	a.ref_crc = d_rcrc.as<uint64_t>();
-	if (dg::launch_decode(a, st) != hipSuccess) return DG_ERR_HIP;
-	// 3. CRC of every output and the dst check (main.c:376-385)
-	if (!ignore_hash) {
-		std::vector<uint64_t> lens(n);
-		if (hipMemcpyAsync(lens.data(), d_out_len, 8ull * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-		    hipStreamSynchronize(st) != hipSuccess)
-			return DG_ERR_HIP;
-		std::vector<dg_span_t> sp(n);
-		for (uint32_t i = 0; i < n; ++i) sp[i] = dg_span_t{descs[i].out_off, lens[i]};
-		int rc = dg_crc64_xz_batch_device(ctx, d_out, sp.data(), n, d_ocrc.as<uint64_t>(), st);
-		if (rc) return rc;
-		if (dg::launch_decode_verify(d_delta, a.descs, n, d_ocrc.as<uint64_t>(), d_status, st) != hipSuccess)
-			return DG_ERR_HIP;
-	}
-	return hipStreamSynchronize(st) == hipSuccess ? DG_OK : DG_ERR_HIP;
+	rc = dg_decode_plan_run(plan, d_ref, d_delta, d_out, d_out_len, d_status, st);
+	if (rc == DG_OK && hipStreamSynchronize(st) != hipSuccess) rc = DG_ERR_HIP;
+	dg_decode_plan_destroy(plan);
+	return rc;
 }
 
 extern "C" int dg_decode(dg_context_t* ctx, const uint8_t* r, size_t r_len, const uint8_t* delta,

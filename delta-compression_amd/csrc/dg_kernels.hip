@@ -485,16 +485,15 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	if (!st) {
 		inplace = D[4] & 1;
 		vsize = be32(D + 5);
-		if (!a.ignore_hash) {
-			uint64_t sc = 0;
-			for (int k = 0; k < 8; ++k) sc = (sc << 8) | D[9 + k];
-			if (sc != a.ref_crc[i]) st = 9;
-		}
 	}
 	const uint64_t bsz = inplace ? max(rl, vsize) : vsize;
 	if (!st && bsz > dd.out_cap) st = 7;
 	if (st) {
-		if (lane == 0) { a.status[i] = st; a.out_len[i] = 0; }
+		if (lane == 0) {
+			a.status[i] = st;
+			a.out_len[i] = 0;
+			if (a.out_spans) a.out_spans[i].len = 0;
+		}
 		return;
 	}
 	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
@@ -612,20 +611,30 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	if (lane == 0) {
 		a.status[i] = st;
 		a.out_len[i] = st ? 0 : vsize;
+		if (a.out_spans) a.out_spans[i].len = st ? 0 : vsize;
 	}
 }
 
-// dst CRC check after the output CRC pass (main.c:379-385)
+// CRC checks after decoding, in the reference's order of precedence: a
+// malformed stream (set by the decoder) first, then the source pre-check
+// (main.c:341-356), then the output post-check (main.c:379-385).  Either CRC
+// array may be null (--ignore-hash).  On a source mismatch the reference stops
+// before applying; here the output buffer content is unspecified.
 __global__ __launch_bounds__(64) void decode_verify_kernel(const uint8_t* delta,
                                                            const dg_decode_desc_dev* descs,
-                                                           uint32_t n, const uint64_t* out_crc,
+                                                           uint32_t n, const uint64_t* ref_crc,
+                                                           const uint64_t* out_crc,
                                                            int32_t* status) {
 	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
 	if (i >= n || status[i] != 0) return;
 	const uint8_t* D = delta + descs[i].delta_off;
-	uint64_t dc = 0;
-	for (int k = 0; k < 8; ++k) dc = (dc << 8) | D[17 + k];
-	if (dc != out_crc[i]) status[i] = 10;
+	uint64_t sc = 0, dc = 0;
+	for (int k = 0; k < 8; ++k) {
+		sc = (sc << 8) | D[9 + k];
+		dc = (dc << 8) | D[17 + k];
+	}
+	if (ref_crc && sc != ref_crc[i]) status[i] = 9;
+	else if (out_crc && dc != out_crc[i]) status[i] = 10;
 }
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
@@ -634,8 +643,11 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
-                                const uint64_t* out_crc, int32_t* status, hipStream_t st) {
-	if (n) hipLaunchKernelGGL(decode_verify_kernel, dim3((n + 63) / 64), dim3(64), 0, st, delta, descs, n, out_crc, status);
+                                const uint64_t* ref_crc, const uint64_t* out_crc, int32_t* status,
+                                hipStream_t st) {
+	if (n)
+		hipLaunchKernelGGL(decode_verify_kernel, dim3((n + 63) / 64), dim3(64), 0, st, delta, descs, n,
+		                   ref_crc, out_crc, status);
 	return hipGetLastError();
 }
 

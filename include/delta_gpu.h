@@ -235,6 +235,27 @@ int dg_decode_batch_device(dg_context_t *ctx, const uint8_t *d_ref,
                            uint64_t *d_out_len, int32_t *d_status,
                            void *stream);
 
+/* Plan form of the batched decode (C5): descriptors uploaded and CRC
+ * segmentation planned once; dg_decode_plan_run is asynchronous device work
+ * only (no host synchronisation, graph-capturable).  The reference CRCs run
+ * on a plan-owned side stream joined before the verify step; the output CRC
+ * spans take their lengths from the delta headers on the device.  Status
+ * precedence per stream: DG_ERR_MALFORMED / DG_ERR_CAPACITY, then
+ * DG_ERR_SRC_CRC, then DG_ERR_DST_CRC (main.c:335-385).  Arena base pointers
+ * d_ref and d_out must be 16-byte aligned.  Timing as for the encode plan;
+ * stage names "ref_crc", "decode", "out_crc+verify", "total". */
+typedef struct dg_decode_plan dg_decode_plan_t;
+int dg_decode_plan_create(dg_context_t *ctx, const dg_decode_desc_t *descs,
+                          uint32_t n, int ignore_hash,
+                          dg_decode_plan_t **out);
+int dg_decode_plan_run(dg_decode_plan_t *plan, const uint8_t *d_ref,
+                       const uint8_t *d_delta, uint8_t *d_out,
+                       uint64_t *d_out_len, int32_t *d_status, void *stream);
+int dg_decode_plan_set_timing(dg_decode_plan_t *plan, int slots);
+int dg_decode_plan_stage_times(dg_decode_plan_t *plan, float *ms,
+                               const char **names, int n);
+void dg_decode_plan_destroy(dg_decode_plan_t *plan);
+
 /* ── delta inspection (host parse, src/c/main.c:402-425) ─────────────── */
 
 typedef struct {

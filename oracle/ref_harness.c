@@ -72,16 +72,42 @@ size_t ref_encode_pair_inplace(int algo, const uint8_t *r, size_t r_len,
 	return b.len;
 }
 
+/* main.c:339-385 in memory: delta_decode, the source CRC pre-check, apply
+ * (standard or in-place), the output CRC post-check.  Returns 0, or 9 / 10
+ * for a source / output CRC mismatch; *out receives the output. */
+int ref_decode_pair(const uint8_t *r, size_t r_len, const uint8_t *delta,
+                    size_t dl, uint8_t **out, size_t *out_len)
+{
+	delta_decode_result_t dr = delta_decode(delta, dl);
+	uint8_t c[DELTA_CRC_SIZE];
+	delta_crc64_xz(r, r_len, c);
+	if (memcmp(c, dr.src_crc, DELTA_CRC_SIZE) != 0) {
+		delta_decode_result_free(&dr);
+		return 9;
+	}
+	delta_buffer_t b = dr.inplace
+	    ? delta_apply_delta_inplace(r, r_len, &dr.commands, dr.version_size)
+	    : delta_apply_placed(r, &dr.commands, dr.version_size);
+	delta_crc64_xz(b.data, dr.version_size, c);
+	int rc = memcmp(c, dr.dst_crc, DELTA_CRC_SIZE) != 0 ? 10 : 0;
+	delta_decode_result_free(&dr);
+	*out = b.data;
+	*out_len = dr.version_size;
+	return rc;
+}
+
 void ref_free(void *p) { free(p); }
 
 #ifdef REF_BENCH_MAIN
 /* ── CPU baseline ───────────────────────────────────────────────────────── */
 
 typedef struct {
-	int algo;
+	int algo;               /* 1 onepass, 2 correcting; 11 / 12: decode standard / in-place onepass deltas */
 	size_t n_pairs, len, p, q;
 	uint8_t **r, **v;
 	size_t *lens;           /* per pair |R| = |V| */
+	uint8_t **d;            /* decode modes: the deltas */
+	size_t *dlens;
 	size_t next;
 	pthread_mutex_t mu;
 	unsigned long long out_bytes;
@@ -97,9 +123,16 @@ static void *worker(void *arg)
 		pthread_mutex_unlock(&j->mu);
 		if (i >= j->n_pairs) break;
 		uint8_t *d = NULL;
-		ob += ref_encode_pair(j->algo, j->r[i], j->lens[i], j->v[i], j->lens[i],
-		                      j->p, j->q, DELTA_BUF_CAP,
-		                      DELTA_MAX_TABLE_SIZE, &d);
+		if (j->algo >= 10) {
+			size_t ol = 0;
+			if (ref_decode_pair(j->r[i], j->lens[i], j->d[i], j->dlens[i], &d, &ol) != 0)
+				abort();
+			ob += ol;
+		} else {
+			ob += ref_encode_pair(j->algo, j->r[i], j->lens[i], j->v[i], j->lens[i],
+			                      j->p, j->q, DELTA_BUF_CAP,
+			                      DELTA_MAX_TABLE_SIZE, &d);
+		}
 		free(d);
 	}
 	pthread_mutex_lock(&j->mu);
@@ -116,6 +149,8 @@ static double now(void)
 }
 
 /* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps
+ * algo 1 / 2: encode onepass / correcting; 11 / 12: decode (+ both CRC checks)
+ * of standard / in-place (localmin) onepass deltas, rate = sum |V| / time;
  * edit_rate >= 0: C2/C3 substitution pairs; edit_rate < 0: C4 transposition
  * pairs (num_blocks = 8 + i mod 57, -edit_rate percent of blocks moved). */
 int main(int argc, char **argv)
@@ -160,6 +195,18 @@ int main(int argc, char **argv)
 	{   /* warm the reference's lazy CRC table before threads start */
 		uint8_t c[8];
 		delta_crc64_xz(j.r[0], 1, c);
+	}
+	if (j.algo >= 10) {   /* decode modes: encode every pair first (untimed) */
+		j.d = malloc(j.n_pairs * sizeof(uint8_t *));
+		j.dlens = malloc(j.n_pairs * sizeof(size_t));
+		total_in = 0;
+		for (size_t i = 0; i < j.n_pairs; i++) {
+			j.dlens[i] = j.algo == 12
+			    ? ref_encode_pair_inplace(1, j.r[i], j.lens[i], j.v[i], j.lens[i], j.p, j.q, 0, &j.d[i])
+			    : ref_encode_pair(1, j.r[i], j.lens[i], j.v[i], j.lens[i], j.p, j.q,
+			                      DELTA_BUF_CAP, DELTA_MAX_TABLE_SIZE, &j.d[i]);
+			total_in += (double)j.lens[i];   /* decode rate counts |V| reconstructed */
+		}
 	}
 	double best = 1e30, sum = 0;
 	unsigned long long out_bytes = 0;

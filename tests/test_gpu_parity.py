@@ -250,3 +250,63 @@ def test_golden_inplace_decode_on_device(dg, ctx, orc):
         R, V = inplace_inputs(orc, c)
         d = bytes.fromhex(c["delta_hex"])
         assert dg.decode(R, d, ctx=ctx) == V, c["name"]
+
+
+def test_decode_plan_batch_mixed(dg, ctx, orc, torch_cuda):
+    """dg_decode_plan over a batch mixing standard and in-place deltas with
+    corrupted ones: per-stream status precedence malformed > src CRC > dst CRC
+    (main.c:335-385), good streams reconstructed exactly, run twice (the plan
+    is reusable and needs no host synchronisation between its kernels)."""
+    import json
+    torch = torch_cuda
+    from test_oracle import inplace_inputs
+    here = os.path.dirname(os.path.abspath(__file__))
+    ip = json.load(open(os.path.join(here, "golden", "golden_inplace.json")))["cases"][:12]
+    items = []   # (R, delta, expected V or None, expected status)
+    for c in ip:
+        R, V = inplace_inputs(orc, c)
+        items.append((R, bytes.fromhex(c["delta_hex"]), V, 0))
+    rng = random.Random(11)
+    for k in range(12):
+        R = rng.randbytes(rng.choice([0, 10, 5000, 70000]))
+        V = R[: len(R) // 2] + rng.randbytes(300) + R[len(R) // 2:]
+        d = orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q)
+        items.append((R, d, V, 0))
+        if k % 3 == 0:
+            items.append((R + b"!", d, None, 9))                      # wrong source
+        if k % 3 == 1:
+            bad = bytearray(d); bad[17] ^= 0x40
+            items.append((R, bytes(bad), None, 10))                  # wrong dst CRC
+        if k % 3 == 2:
+            items.append((R, d[:25] + b"\x07" + d[26:], None, 8))     # bad command tag
+            items.append((R + b"!", b"DLT\x02" + d[4:], None, 8))    # magic beats src CRC
+    up = lambda x: (x + 15) // 16 * 16
+    r_off, d_off, o_off, descs = 0, 0, 0, []
+    for R, d, V, _ in items:
+        vs = int.from_bytes(d[5:9], "big") if len(d) >= 9 else 0
+        cap = max(vs, len(R), 1)
+        descs.append((r_off, len(R), d_off, len(d), o_off, cap))
+        r_off += up(len(R)); d_off += len(d); o_off += up(cap)
+    ref = torch.zeros(max(r_off, 16), dtype=torch.uint8)
+    dl = torch.zeros(max(d_off, 16), dtype=torch.uint8)
+    for (R, d, _, _), (ro, rl, do, dln, _, _) in zip(items, descs):
+        if rl:
+            ref[ro:ro + rl] = torch.frombuffer(bytearray(R), dtype=torch.uint8)
+        dl[do:do + dln] = torch.frombuffer(bytearray(d), dtype=torch.uint8)
+    ref, dl = ref.cuda(), dl.cuda()
+    out = torch.zeros(max(o_off, 16), dtype=torch.uint8, device="cuda")
+    olen = torch.zeros(len(items), dtype=torch.int64, device="cuda")
+    st = torch.zeros(len(items), dtype=torch.int32, device="cuda")
+    plan = dg.DecodePlan(ctx, descs)
+    for _ in range(2):
+        out.zero_()
+        torch.cuda.synchronize()
+        plan.run(ref.data_ptr(), dl.data_ptr(), out.data_ptr(), olen.data_ptr(), st.data_ptr(),
+                 ctx.stream)
+        torch.cuda.synchronize()
+        stc, oc, lc = st.cpu().tolist(), out.cpu(), olen.cpu().tolist()
+        for i, ((R, d, V, want), ds) in enumerate(zip(items, descs)):
+            assert stc[i] == want, (i, stc[i], want)
+            if want == 0:
+                assert lc[i] == len(V)
+                assert bytes(oc[ds[4]:ds[4] + len(V)].numpy()) == V, i
