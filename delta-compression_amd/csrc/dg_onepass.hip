@@ -61,7 +61,7 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #ifdef DG_ONEPASS_PROF
 enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATCH, P_B_ENTRIES,
        P_B_CHUNKS, P_C_CHUNKS, P_EXTENDS, P_REFILLS, P_T_DIAG, P_T_A, P_T_BC, P_T_EXT, P_T_REFILL,
-       P_T_TOTAL, P_B_WALKED, kProfN };
+       P_T_TOTAL, P_B_WALKED, P_T_D1, P_T_D2, P_T_D3, P_T_D4, P_D_MEMBERS, P_D_STEPS, P_T_D3A, P_T_D3B, kProfN };
 __device__ unsigned long long g_onepass_prof[kProfN];
 #define PROF_DECL uint64_t prof[kProfN];
 #define PROF_INIT(o) for (int _i = 0; _i < kProfN; ++_i) (o).prof[_i] = 0;
@@ -86,11 +86,63 @@ __device__ __forceinline__ uint32_t dpp_xor1(uint32_t x) {
 __device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
 	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
 }
+// lane l receives x of lane l-1 (lane 0: 0) — DPP wave_shr:1, no LDS
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+}
+// inclusive prefix sum over the wave: row_shr 1/2/4/8 inside rows of 16, then
+// row_bcast:15 / row_bcast:31 across rows (all DPP, no LDS round trips)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+	return x;
+}
+
 __device__ __forceinline__ uint64_t quad_sum64(uint64_t x) {
 	uint64_t y = ((uint64_t)dpp_xor1((uint32_t)(x >> 32)) << 32) | dpp_xor1((uint32_t)x);
 	x += y;
 	y = ((uint64_t)dpp_xor2((uint32_t)(x >> 32)) << 32) | dpp_xor2((uint32_t)x);
 	return x + y;
+}
+
+// p = 16 fingerprints by byte dot products.  fp = sum_k b_k * c_k mod M with
+// c_k = 263^(15-k); splitting every c_k into its 8 bytes gives
+//   fp = sum_j 2^(8j) * D_j,  D_j = sum_k b_k * byte_j(c_k) < 2^20,
+// and each D_j is four v_dot4_u32_u8 over the window's four dwords (zero
+// constant bytes drop out at compile time).  kFpLimb[j][g] packs byte j of
+// c_{4g..4g+3}.
+constexpr uint32_t kFpLimb[8][4] = {
+    {0x90948E99u, 0xCA791EB5u, 0x61A791F7u, 0x01073157u},
+    {0x1E666240u, 0xAE927B7Cu, 0x6526B587u, 0x00010E94u},
+    {0x58871A1Bu, 0xBBD04668u, 0x2B953A50u, 0x00000115u},
+    {0xC9D97A71u, 0x30104632u, 0x1DF75AB2u, 0x00000001u},
+    {0x5F67B04Du, 0x15C57474u, 0x0124FA32u, 0x00000000u},
+    {0xCCF624B1u, 0xA7A654C3u, 0x00012C35u, 0x00000000u},
+    {0x03E64716u, 0xA94AB12Du, 0x00000135u, 0x00000000u},
+    {0x140F1603u, 0x1D191B13u, 0x00000001u, 0x00000000u},
+};
+
+__device__ __forceinline__ uint64_t fp16_dot(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+	const uint32_t w[4] = {w0, w1, w2, w3};
+	uint32_t D[8];
+#pragma unroll
+	for (int j = 0; j < 8; ++j) {
+		uint32_t acc = 0;
+#pragma unroll
+		for (int g = 0; g < 4; ++g)
+			if (kFpLimb[j][g]) acc = __builtin_amdgcn_udot4(w[g], kFpLimb[j][g], acc, false);
+		D[j] = acc;
+	}
+	uint64_t x = (uint64_t)D[0] + ((uint64_t)D[1] << 8) + ((uint64_t)D[2] << 16) +
+	             ((uint64_t)D[3] << 24) + ((uint64_t)D[4] << 32) + ((uint64_t)D[5] << 40);
+	// 2^61 == 1 (mod M): fold what D_6, D_7 carry past bit 61
+	x += ((uint64_t)(D[6] & 0x1FFFu) << 48) + (D[6] >> 13);
+	x += ((uint64_t)(D[7] & 0x1Fu) << 56) + (D[7] >> 5);
+	return mod_m61(x);
 }
 
 __device__ __forceinline__ uint64_t fold61(uint64_t lo, uint64_t hi) {
@@ -206,19 +258,7 @@ struct WinSrc {
 	}
 
 	__device__ __forceinline__ uint64_t fp16(uint32_t s, uint32_t x) const {
-		uint64_t lo = 0, hi = 0;
-#pragma unroll
-		for (int g = 0; g < 4; ++g) {
-			const uint32_t w = rd4(s, x + 4 * g);
-#pragma unroll
-			for (int j = 0; j < 4; ++j) {
-				const uint64_t c = powc[4 * g + j];
-				const uint64_t b = (w >> (8 * j)) & 0xff;
-				lo += b * (uint32_t)c;
-				hi += b * (uint32_t)(c >> 32);
-			}
-		}
-		return fold61(lo, hi);
+		return fp16_dot(rd4(s, x), rd4(s, x + 4), rd4(s, x + 8), rd4(s, x + 12));
 	}
 
 	// windows for a 64-step chunk starting at (vpos, rpos)
@@ -231,29 +271,38 @@ struct WinSrc {
 	// ── diagonal batch ──────────────────────────────────────────────────
 	// State (v0, r0) sits on a mismatch (V[v0] != R[r0]) left by the previous
 	// extension.  Let a_0 = 0 < a_1 < ... be the mismatch offsets along the
-	// diagonal (plus the stream end as a terminator) within the next 1 KiB.
-	// Epoch i starts at (v0+a_i, r0+a_i).  Its step 0 cannot match (first
-	// bytes differ).  If a_{i+1} - a_i >= 17, step 1's windows are equal, and
-	// step 1 resolves as the reference would iff
-	//   slotV0 != slotR1                          (lookup 1 finds s = 1), or
-	//   fpV0 != fpR1 and slotR0 != slotV1         (lookup 1's s = 0 fails
-	//                                              memcmp; lookup 2 finds s = 1)
-	// in which case the epoch emits ADD(1 byte) + COPY(a_i+1 .. a_{i+1}).
-	// Four lanes per epoch compute the four window slots; the first epoch
-	// that does not qualify ends the batch and goes through the exact path.
-	// Returns the number of epochs committed; *adv = offset of the new state.
+	// diagonal within the next 1 KiB (the end of the shorter stream counts as
+	// one).  An epoch starting at a_k first sees equal windows at step
+	//   T_k = a_m + 1 - a_k,  m = the first index >= k with a_{m+1} - a_m > p,
+	// and, if it resolves there on the diagonal, emits ADD(T_k bytes) +
+	// COPY(a_k + T_k .. a_{m+1}) and hands over to the epoch at a_{m+1}.  The
+	// chain of such epochs is laid out over the lanes (one lane per step of
+	// each epoch, at most 64 steps in all) and each epoch is checked exactly
+	// against the reference's lookups (onepass.c:169-219):
+	//   step t < T_k:  neither lookup may verify.  The diagonal candidate
+	//                  (s = t) differs in its bytes by construction; an earlier
+	//                  candidate (s < t) must differ in its fingerprint —
+	//                  equal fingerprints (a possible genuine match elsewhere)
+	//                  end the batch and the exact path takes the epoch;
+	//   step T_k:      lookup 1 must find s = T_k, or fail on the fingerprint
+	//                  with lookup 2 then finding s = T_k.
+	// "Earliest s" is the reference's first-writer slot (HV/HR hold the first
+	// step of the epoch that hashed to the slot).  The epochs before the first
+	// one that fails the check are committed.  Returns the number committed;
+	// *adv = offset of the new state, *more = the batch ended only because the
+	// chain left the known region (another batch can follow directly),
+	// *dsz_add = their delta bytes.
 	__device__ uint32_t diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
-	                               uint64_t qmag, uint32_t* rec, uint32_t nrec, uint32_t rec_cap,
-	                               uint32_t* mlist, uint32_t* adv, uint32_t* npred) {
+	                               uint64_t qmag, uint32_t p, uint32_t* rec, uint32_t nrec,
+	                               uint32_t rec_cap, uint32_t* mlist, uint32_t* adv, bool* more,
+	                               uint32_t* dsz_add) {
 		const uint32_t lane = lane_id();
 		const uint32_t lim = umin32(vl - v0, rl - r0);
-		*npred = 0;
 		*adv = 0;
-		// epoch 0 qualifies only if bytes 1..16 agree: check them first (cheap)
-		if (lim < 17) return 0;
-		ensure2(v0, r0, 24, true, true);
-		const uint32_t x0 = lane < 4 ? (rd4(0, v0 + 1 + 4 * lane) ^ rd4(1, r0 + 1 + 4 * lane)) : 0u;
-		if (__ballot(x0 != 0)) return 0;
+		*more = false;
+		*dsz_add = 0;
+		if (lim < p + 1) return 0;
+		[[maybe_unused]] uint64_t tq = PROF_NOW();
 		ensure2(v0, r0, 1024 + 48, true, true);
 		// 1. mismatch bits of offsets [16*lane, 16*lane+16)
 		const uint32_t base = 16 * lane;
@@ -270,51 +319,115 @@ struct WinSrc {
 		}
 		// 2. ordered list of mismatch offsets (exclusive prefix of counts)
 		const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
-		uint32_t incl = cnt;
-#pragma unroll
-		for (int d = 1; d < 64; d <<= 1) {
-			const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-			if (lane >= (uint32_t)d) incl += y;
-		}
+		const uint32_t incl = wave_incl_scan(cnt);
 		uint32_t pos = incl - cnt;
 		const uint32_t total = rdlane(incl, 63);
 		for (uint32_t b = bits; b && pos < 64; b &= b - 1, ++pos) mlist[pos] = base + __builtin_ctz(b);
 		__builtin_amdgcn_s_waitcnt(0xc07f);
 		__builtin_amdgcn_wave_barrier();
 		const uint32_t K = umin32(total, 64u);
-		const uint32_t E = K > 1 ? umin32(K - 1, 16u) : 0u;
-		*npred = E;
-		*adv = 0;
-		if (E == 0) return 0;
-		// 3. the four windows of each predicted epoch
-		const uint32_t i = lane >> 2, w = lane & 3u;
-		const bool act = i < E;
-		const uint32_t ai = act ? mlist[i] : 0u;
-		const uint32_t g = act ? mlist[i + 1] - ai : 0u;
-		const uint32_t s = w >> 1;
-		const uint64_t fp = fp16(s, (s ? r0 : v0) + ai + (w & 1u));
-		const uint32_t slot = (uint32_t)mod_q(fp, q, qmag);
-		const uint32_t fpl = (uint32_t)fp;
-		const uint32_t sV0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0x00, 0xF, 0xF, false);
-		const uint32_t sV1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0x55, 0xF, 0xF, false);
-		const uint32_t sR0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0xAA, 0xF, 0xF, false);
-		const uint32_t sR1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)slot, 0xFF, 0xF, 0xF, false);
-		const uint32_t fV0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpl, 0x00, 0xF, 0xF, false);
-		const uint32_t fR1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fpl, 0xFF, 0xF, 0xF, false);
-		const bool ok = act && g >= 17 && (sV0 != sR1 || (fV0 != fR1 && sR0 != sV1));
-		const uint64_t heads = 0x1111111111111111ull & ((E >= 16) ? ~0ull : ((1ull << (4 * E)) - 1ull));
-		const uint64_t bad = heads & ~__ballot(ok);
-		uint32_t f = bad ? (ffs64(bad) >> 2) : E;
-		if (nrec + f > rec_cap) f = 0;
-		// 4. commit epochs 0..f-1: ADD V[a_i] (1 byte) + COPY(a_i+1, a_{i+1}-a_i-1)
-		if (w == 0 && i < f) {
-			uint32_t* o = rec + 3u * (nrec + i);
-			o[0] = v0 + ai + 1;
-			o[1] = r0 + ai + 1;
-			o[2] = g - 1;
+		if (K < 2) return 0;
+		PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
+		tq = PROF_NOW();
+		const uint32_t ak = lane < K ? mlist[lane] : 0xFFFFFFFFu;
+		const uint32_t an = lane + 1 < K ? mlist[lane + 1] : 0xFFFFFFFFu;
+		const uint64_t G = __ballot(lane + 1 < K && an - ak > p);   // a long gap follows a_lane
+		// 3. the chain of epochs (scalar): member j starts at a_cur, first
+		//    equal step T, ends at a_{m+1}; steps laid out from lane B
+		uint32_t cur = 0, B = 0, nm = 0, sumT = 0, maxT = 0;
+		uint64_t starts = 0;
+		uint32_t mstart = 0, mT = 0, mend = 0, mcumT = 0;   // lane j: member j
+		while (nm < 64 && cur + 1 < K) {
+			const uint64_t Gs = G >> cur;
+			if (!Gs) break;
+			const uint32_t m = cur + ffs64(Gs);
+			const uint32_t a0 = rdlane(ak, cur);
+			const uint32_t T = rdlane(ak, m) + 1 - a0;
+			if (T > 63 || B + T + 1 > 64) break;
+			mstart = lane == nm ? a0 : mstart;
+			mT = lane == nm ? T : mT;
+			mend = lane == nm ? rdlane(ak, m + 1) : mend;
+			mcumT = lane == nm ? sumT : mcumT;
+			starts |= 1ull << B;
+			maxT = umax32(maxT, T);
+			B += T + 1;
+			sumT += T;
+			++nm;
+			cur = m + 1;
 		}
-		*adv = mlist[f];
-		return f;
+		if (nm == 0) return 0;
+		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
+		PROF_ADD(*this, P_D_MEMBERS, nm);
+		PROF_ADD(*this, P_D_STEPS, B);
+		tq = PROF_NOW();
+		// 4. windows of every step: lane f is step t of member j
+		const bool live = lane < B;
+		const uint64_t below = starts & mask_le(lane);
+		const uint32_t j = live ? (uint32_t)__builtin_popcountll(below) - 1u : 0u;
+		const uint32_t fb = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;   // member's first lane
+		const uint32_t t = lane - fb;
+		const uint32_t js = (uint32_t)__shfl((int)mstart, (int)j, 64);
+		const uint32_t jT = (uint32_t)__shfl((int)mT, (int)j, 64);
+		uint32_t sV = kSentinel, sR = kSentinel - 1u, fVl = 0, fRl = 0;
+		PROF_ADD(*this, P_T_D3A, PROF_NOW() - tq);
+		if (live) {
+			const uint64_t fV = fp16(0, v0 + js + t), fR = fp16(1, r0 + js + t);
+			sV = (uint32_t)mod_q(fV, q, qmag);
+			sR = (uint32_t)mod_q(fR, q, qmag);
+			fVl = (uint32_t)fV;
+			fRl = (uint32_t)fR;
+		}
+		// 5. first writers: s1 = first lane c in [fb, lane] with sV(c) == sR(lane),
+		//    s2 = first with sR(c) == sV(lane)
+		PROF_ADD(*this, P_T_D3B, PROF_NOW() - tq);
+		//    Lane l looks back d = 0 .. t lanes (its own member's earlier
+		//    steps) through DPP wave shifts; the largest matching d is the
+		//    earliest writer, whose fingerprint rides along.
+		uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
+		{
+			uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
+			for (uint32_t d = 0; d <= maxT; ++d) {
+				if (d) {
+					xv = wave_shr1(xv);
+					xr = wave_shr1(xr);
+					xfv = wave_shr1(xfv);
+					xfr = wave_shr1(xfr);
+				}
+				if (d <= t) {
+					if (xv == sR) { s1 = lane - d; f1 = xfv; }
+					if (xr == sV) { s2 = lane - d; f2 = xfr; }
+				}
+			}
+		}
+		PROF_ADD(*this, P_T_D3, PROF_NOW() - tq);
+		tq = PROF_NOW();
+		// 6. the reference's resolution of step t
+		bool bad = false, hit = false;
+		if (s1 != 64) {
+			if (s1 == lane) hit = t == jT;          // the diagonal: equal bytes iff t == T
+			else if (f1 == fRl) bad = true;         // a possible match off the diagonal
+		}
+		if (!hit && !bad && s2 != 64) {
+			if (s2 == lane) hit = t == jT;
+			else if (f2 == fVl) bad = true;
+		}
+		if (t == jT && !hit) bad = true;            // the epoch would go on past T
+		const uint64_t BM = __ballot(live && bad);
+		uint32_t fm = BM ? (uint32_t)__builtin_popcountll(starts & mask_le(ffs64(BM))) - 1u : nm;
+		if (nrec + fm > rec_cap) fm = 0;
+		// 7. commit members 0 .. fm-1: ADD(T bytes) + COPY(a + T .. end)
+		if (lane < fm) {
+			uint32_t* o = rec + 3u * (nrec + lane);
+			o[0] = v0 + mstart + mT;
+			o[1] = r0 + mstart + mT;
+			o[2] = mend - mstart - mT;
+		}
+		const uint32_t cumT = fm < nm ? rdlane(mcumT, fm) : sumT;
+		*dsz_add = 22u * fm + cumT;
+		*adv = fm < nm ? rdlane(mstart, fm) : rdlane(mend, nm - 1);
+		*more = fm == nm;
+		PROF_ADD(*this, P_T_D4, PROF_NOW() - tq);
+		return fm;
 	}
 
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
@@ -372,10 +485,11 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 		if (v0 + p > vl || r0 + p > rl) break;
 		if constexpr (Src::kPhaseA) {
 			if (at_mismatch) {
-				uint32_t adv = 0, npred = 0;
+				uint32_t adv = 0, dadd = 0;
+				bool more = false;
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
-				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, rec, nrec, rec_cap, bm,
-				                                      &adv, &npred));
+				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, p, rec, nrec, rec_cap, bm,
+				                                      &adv, &more, &dadd));
 				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
 				PROF_ADD(src, P_DIAG_CALLS, 1);
 				PROF_ADD(src, P_DIAG_EPOCHS, f);
@@ -383,10 +497,10 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 				if (f) {
 					adv = uni(adv);
 					nrec += f;
-					dsz += 23ull * f;   // per epoch: ADD 9+1 B, COPY 13 B
+					dsz += uni(dadd);
 					v0 += adv;
 					r0 += adv;
-					if (f == uni(npred)) continue;   // all predicted: next batch
+					if (uni((uint32_t)more)) continue;   // the chain left the region: next batch
 					if (v0 + p > vl || r0 + p > rl) break;
 				}
 			}

@@ -15,7 +15,8 @@ sys.path.insert(0, ROOT)
 
 NAMES = ["epochs", "diag_calls", "diag_epochs", "diag_zero", "a_entries", "a_match", "b_entries",
          "b_chunks", "c_chunks", "extends", "refills", "t_diag", "t_a", "t_bc", "t_ext", "t_refill",
-         "t_total", "b_walked"]
+         "t_total", "b_walked", "t_d1_list", "t_d2_chain", "t_d3_fp_lookup", "t_d4_resolve", "d_members",
+         "d_steps", "t_d3a_map", "t_d3ab_map_fp"]
 
 
 def main():
@@ -31,7 +32,7 @@ def main():
     L_.dg_onepass_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     L_.dg_onepass_prof_reset.argtypes = []
     ctx = dg.Context(0)
-    npg, L, rate, q, seed, _ = CONFIGS[args.config]
+    npg, L, rate, q, seed = CONFIGS[args.config][:5]
     n = args.pairs or npg
     ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
