@@ -39,6 +39,7 @@ from ._lib import (  # noqa: F401
     encode_batch,
     info,
     lib,
+    make_inplace,
     status_string,
 )
 
@@ -46,5 +47,5 @@ __all__ = [
     "ALGO_ONEPASS", "ALGO_CORRECTING", "ALGO_GREEDY", "SEED_LEN", "TABLE_SIZE",
     "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan", "DecodePlan",
     "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
-    "status_string", "LIB_PATH",
+    "make_inplace", "status_string", "LIB_PATH",
 ]

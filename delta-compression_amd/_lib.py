@@ -21,7 +21,8 @@ SEED_LEN = 16
 TABLE_SIZE = 1048573
 MAX_TABLE_SIZE = 1073741827
 BUF_CAP = 256
-OPT_VERBOSE, OPT_SPLAY, OPT_INPLACE = 0, 1, 2
+OPT_VERBOSE, OPT_SPLAY, OPT_INPLACE, OPT_POLICY_CONSTANT = 0, 1, 2, 3
+POLICIES = {"localmin": 0, "constant": 1}
 
 _ALGOS = {"greedy": ALGO_GREEDY, "onepass": ALGO_ONEPASS, "correcting": ALGO_CORRECTING}
 
@@ -66,6 +67,11 @@ class DecodeDesc(C.Structure):
     _fields_ = [("ref_off", C.c_uint64), ("ref_len", C.c_uint64),
                 ("delta_off", C.c_uint64), ("delta_len", C.c_uint64),
                 ("out_off", C.c_uint64), ("out_cap", C.c_uint64)]
+
+
+class InplaceStats(C.Structure):
+    _fields_ = [("already_inplace", C.c_int), ("num_copies", C.c_uint64), ("num_adds", C.c_uint64),
+                ("copy_bytes", C.c_uint64), ("add_bytes", C.c_uint64)]
 
 
 class DeltaInfo(C.Structure):
@@ -132,6 +138,7 @@ def _load() -> C.CDLL:
         "dg_decode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
         "dg_decode_plan_destroy": (None, [vp]),
         "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
+        "dg_make_inplace": (C.c_int, [u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer), C.POINTER(InplaceStats)]),
         "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
         "dg_synth_transpose_pairs_device": (C.c_int, [vp, u64, u32, u64, u32, C.POINTER(Pair),
                                                       C.POINTER(u64), C.POINTER(u64), vp, vp, vp]),
@@ -155,8 +162,9 @@ def _u8(b: bytes):
 
 
 def _opts(p=SEED_LEN, q=TABLE_SIZE, buf_cap=BUF_CAP, max_table=MAX_TABLE_SIZE, flags=0,
-          verbose=False, splay=False, inplace=False) -> DiffOptions:
+          verbose=False, splay=False, inplace=False, policy="localmin") -> DiffOptions:
     f = flags | (verbose << OPT_VERBOSE) | (splay << OPT_SPLAY) | (inplace << OPT_INPLACE)
+    f |= POLICIES[policy] << OPT_POLICY_CONSTANT
     return DiffOptions.make(p, q, buf_cap, max_table, f)
 
 
@@ -308,11 +316,12 @@ class DecodePlan:
 
 def encode(R: bytes, V: bytes, algorithm="onepass", p: int = SEED_LEN, q: int = TABLE_SIZE,
            buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE, splay: bool = False,
-           inplace: bool = False, ctx: Optional[Context] = None) -> bytes:
+           inplace: bool = False, policy: str = "localmin",
+           ctx: Optional[Context] = None) -> bytes:
     """One pair, host bytes in, DLT\\x03 bytes out (src/c/main.c:257-292)."""
     ctx = ctx or default_context()
     out = Buffer()
-    o = _opts(p, q, buf_cap, max_table, splay=splay, inplace=inplace)
+    o = _opts(p, q, buf_cap, max_table, splay=splay, inplace=inplace, policy=policy)
     rc = lib.dg_encode(ctx.handle, _algo(algorithm), _u8(R), len(R), _u8(V), len(V), C.byref(o),
                        C.byref(out))
     ctx.check(rc, "dg_encode")
@@ -345,6 +354,21 @@ def encode_batch(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: i
             raise DeltaError(st[i], f"pair {i}")
         res.append(C.string_at(outs[i].data, outs[i].len))
         lib.dg_buffer_free(C.byref(outs[i]))
+    return res
+
+
+def make_inplace(R: bytes, delta: bytes, policy: str = "localmin", stats: bool = False):
+    """main.c `inplace` (:427-480): standard delta -> in-place delta, host only."""
+    out = Buffer()
+    st = InplaceStats()
+    rc = lib.dg_make_inplace(_u8(R), len(R), _u8(delta), len(delta), POLICIES[policy], C.byref(out),
+                             C.byref(st))
+    if rc:
+        raise DeltaError(rc, "dg_make_inplace")
+    res = C.string_at(out.data, out.len) if out.len else b""
+    lib.dg_buffer_free(C.byref(out))
+    if stats:
+        return res, {k: getattr(st, k) for k, _ in InplaceStats._fields_}
     return res
 
 

@@ -9,9 +9,11 @@
  *   delta encode <onepass|correcting> <ref> <ver> <delta> [options]
  *   delta decode <ref> <delta> <output> [--ignore-hash]
  *   delta info <delta>
+ *   delta inplace <ref> <delta_in> <delta_out> [--policy localmin|constant]
  *
- * Not provided by this build (exit 1 with a message): the greedy algorithm,
- * --splay, --inplace / the inplace subcommand (CRWI conversion).
+ * --inplace / inplace run the CRWI conversion on the host (dg_make_inplace,
+ * main.c:279-283 and :427-480).  Not provided by this build (exit 1 with a
+ * message): the greedy algorithm and --splay.
  */
 #include <errno.h>
 #include <getopt.h>
@@ -85,6 +87,7 @@ static void usage(void)
 	    "  delta encode <algorithm> <ref> <ver> <delta> [options]\n"
 	    "  delta decode <ref> <delta> <output> [--ignore-hash]\n"
 	    "  delta info <delta>\n"
+	    "  delta inplace <ref> <delta_in> <delta_out> [--policy P]\n"
 	    "\n"
 	    "Algorithms: onepass, correcting (MI355X)\n"
 	    "\n"
@@ -92,6 +95,8 @@ static void usage(void)
 	    "  --seed-len N     Seed length (default %d)\n"
 	    "  --table-size N   Hash table size floor (default %lu)\n"
 	    "  --max-table N    Max hash table size, k/M/B suffix ok (default %lu)\n"
+	    "  --inplace        Produce in-place delta\n"
+	    "  --policy P       Cycle policy: localmin (default), constant\n"
 	    "  --verbose        Print diagnostics\n",
 	    DG_SEED_LEN, (unsigned long)DG_TABLE_SIZE, (unsigned long)DG_MAX_TABLE_SIZE);
 	exit(1);
@@ -124,6 +129,7 @@ static int cmd_encode(int argc, char **argv)
 	}
 	dg_diff_options_t o;
 	dg_diff_options_default(&o);
+	const char *policy_str = "localmin";
 	static struct option lo[] = {
 		{"seed-len", required_argument, NULL, 's'},
 		{"table-size", required_argument, NULL, 't'},
@@ -141,13 +147,14 @@ static int cmd_encode(int argc, char **argv)
 		case 't': o.q = (size_t)atol(optarg); break;
 		case 'x': o.max_table = parse_size_suffix(optarg); break;
 		case 'v': o.flags |= 1ull << DG_OPT_VERBOSE; break;
-		case 'i':
-			fprintf(stderr, "--inplace is not provided by the MI355X build\n");
-			return 1;
+		case 'i': o.flags |= 1ull << DG_OPT_INPLACE; break;
 		case 'y':
 			fprintf(stderr, "--splay is not provided by the MI355X build\n");
 			return 1;
-		case 'p': break;
+		case 'p':
+			policy_str = optarg;
+			if (strcmp(optarg, "constant") == 0) o.flags |= 1ull << DG_OPT_POLICY_CONSTANT;
+			break;
 		default: usage();
 		}
 	}
@@ -169,7 +176,10 @@ static int cmd_encode(int argc, char **argv)
 	write_file(delta_path, d.data, d.len);
 	dg_delta_info_t inf;
 	dg_delta_info(d.data, d.len, &inf);
-	printf("Algorithm:    %s\n", algo_str);
+	if ((o.flags >> DG_OPT_INPLACE) & 1)
+		printf("Algorithm:    %s + in-place (%s)\n", algo_str, policy_str);
+	else
+		printf("Algorithm:    %s\n", algo_str);
 	printf("Reference:    %s (%zu bytes)\n", ref_path, rl);
 	printf("Version:      %s (%zu bytes)\n", ver_path, vl);
 	printf("Delta:        %s (%zu bytes)\n", delta_path, d.len);
@@ -271,16 +281,56 @@ static int cmd_info(int argc, char **argv)
 	return 0;
 }
 
+static int cmd_inplace(int argc, char **argv)   /* main.c:427-480 */
+{
+	if (argc < 5) usage();
+	const char *ref_path = argv[2], *in_path = argv[3], *out_path = argv[4];
+	int policy = DG_POLICY_LOCALMIN;
+	const char *policy_str = "localmin";
+	for (int a = 5; a < argc; a++)
+		if (strcmp(argv[a], "--policy") == 0 && a + 1 < argc) {
+			policy_str = argv[++a];
+			if (strcmp(policy_str, "constant") == 0) policy = DG_POLICY_CONSTANT;
+		}
+	size_t rl, dl;
+	uint8_t *r = read_file(ref_path, &rl), *d = read_file(in_path, &dl);
+	dg_buffer_t o = {0};
+	dg_inplace_stats_t st;
+	double t0 = now();
+	int rc = dg_make_inplace(r, rl, d, dl, policy, &o, &st);
+	double t1 = now();
+	if (rc) {
+		fprintf(stderr, "delta_decode: %s\n",
+		        (dl < DG_HEADER_SIZE || memcmp(d, "DLT\x03", 4)) ? "not a delta file" : dg_status_string(rc));
+		return 1;
+	}
+	write_file(out_path, o.data, o.len);
+	if (st.already_inplace) {
+		printf("Delta is already in-place format; copied unchanged.\n");
+	} else {
+		printf("Reference:    %s (%zu bytes)\n", ref_path, rl);
+		printf("Input delta:  %s (%zu bytes)\n", in_path, dl);
+		printf("Output delta: %s (%zu bytes)\n", out_path, o.len);
+		printf("Format:       in-place (%s)\n", policy_str);
+		printf("Commands:     %llu copies, %llu adds\n", (unsigned long long)st.num_copies,
+		       (unsigned long long)st.num_adds);
+		printf("Copy bytes:   %llu\n", (unsigned long long)st.copy_bytes);
+		printf("Add bytes:    %llu\n", (unsigned long long)st.add_bytes);
+		printf("Time:         %.3fs\n", t1 - t0);
+	}
+	dg_buffer_free(&o);
+	free(r);
+	free(d);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	if (argc < 2) usage();
 	if (strcmp(argv[1], "encode") == 0) return cmd_encode(argc, argv);
 	if (strcmp(argv[1], "decode") == 0) return cmd_decode(argc, argv);
 	if (strcmp(argv[1], "info") == 0) return cmd_info(argc, argv);
-	if (strcmp(argv[1], "inplace") == 0) {
-		fprintf(stderr, "inplace conversion is not provided by the MI355X build\n");
-		return 1;
-	}
+	if (strcmp(argv[1], "inplace") == 0) return cmd_inplace(argc, argv);
 	usage();
 	return 1;
 }

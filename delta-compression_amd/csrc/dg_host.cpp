@@ -327,7 +327,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	if ((o.flags >> DG_OPT_SPLAY) & 1)
 		return set_err(ctx, DG_ERR_UNSUPPORTED, "--splay is not supported (hash-table path only)");
 	if ((o.flags >> DG_OPT_INPLACE) & 1)
-		return set_err(ctx, DG_ERR_UNSUPPORTED, "in-place encode is not supported by the batch path");
+		return set_err(ctx, DG_ERR_UNSUPPORTED,
+		               "in-place conversion is a host step: encode standard deltas, then dg_make_inplace");
 	if (o.p == 0) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len must be >= 1");
 	if (o.p > 65536) return set_err(ctx, DG_ERR_INVALID_ARG, "--seed-len above 65536 is not supported");
 	if (algo == DG_ALGO_CORRECTING && o.buf_cap > 4095)

@@ -47,6 +47,28 @@ int dg_encode_batch(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* const
 	if (!ctx || (n && (!r || !r_len || !v || !v_len || !outs))) return DG_ERR_INVALID_ARG;
 	for (uint32_t i = 0; i < n; ++i) outs[i].data = nullptr, outs[i].len = 0;
 	if (n == 0) return DG_OK;
+	if (opts && ((opts->flags >> DG_OPT_INPLACE) & 1)) {
+		// main.c:279-292 with --inplace: the standard encode on the device,
+		// then delta_make_inplace on the host
+		dg_diff_options_t o = *opts;
+		o.flags &= ~(1ull << DG_OPT_INPLACE);
+		const int policy = ((opts->flags >> DG_OPT_POLICY_CONSTANT) & 1) ? DG_POLICY_CONSTANT : DG_POLICY_LOCALMIN;
+		std::vector<int32_t> st(n, 0);
+		int rc = dg_encode_batch(ctx, algo, r, r_len, v, v_len, n, &o, outs, st.data());
+		if (rc) return rc;
+		int first_bad = DG_OK;
+		for (uint32_t i = 0; i < n; ++i) {
+			if (st[i] == DG_OK && outs[i].data) {
+				dg_buffer_t ip{nullptr, 0};
+				st[i] = dg_make_inplace(r[i], r_len[i], outs[i].data, outs[i].len, policy, &ip, nullptr);
+				free(outs[i].data);
+				outs[i] = ip;
+			}
+			if (status) status[i] = st[i];
+			if (st[i] && !first_bad) first_bad = st[i];
+		}
+		return status ? DG_OK : first_bad;
+	}
 	hipStream_t st = (hipStream_t)dg_context_stream(ctx);
 
 	std::vector<dg_pair_t> pairs(n);

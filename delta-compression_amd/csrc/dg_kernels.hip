@@ -61,13 +61,29 @@ __device__ __forceinline__ void put_u32be(uint8_t* o, uint32_t x) {
 // One 256-thread block per pair.  Commands are in V order with sequential
 // destinations (apply.c:136-164): every gap between consecutive COPYs is one
 // ADD of V bytes, so the COPY records alone describe the delta.
+//
+// Records are taken 256 at a time (one per thread).  A block scan gives each
+// command's offset; the tile's bytes are assembled in LDS (headers by their
+// thread, ADD payloads copied from V by their thread, or by the whole block
+// when long) and then written out as coalesced dwords.  A tile whose bytes do
+// not fit the staging buffer is written directly instead.
+constexpr uint32_t kSerStage = 20480;
+
+__device__ __forceinline__ void put_u32be_lds(uint8_t* o, uint32_t x) {
+	o[0] = (uint8_t)(x >> 24);
+	o[1] = (uint8_t)(x >> 16);
+	o[2] = (uint8_t)(x >> 8);
+	o[3] = (uint8_t)x;
+}
+
 __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 	const uint32_t pair = blockIdx.x;
 	const uint32_t tid = threadIdx.x;
 	__shared__ uint64_t scan[256];
-	__shared__ uint64_t big_dst[256], big_src[256], big_len[256];
+	__shared__ uint32_t big_dst[256], big_src[256], big_len[256];
 	__shared__ uint32_t n_big;
 	__shared__ uint64_t pos_sh;
+	__shared__ __attribute__((aligned(16))) uint8_t stage[kSerStage + 8];
 
 	const uint64_t base = s.offsets[pair];
 	const uint64_t end = s.offsets[pair + 1];
@@ -118,36 +134,88 @@ __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 			__syncthreads();
 		}
 		const uint64_t pos = pos_sh;
-		if (valid) {
-			uint8_t* o = out + pos + scan[tid] - sz;
-			if (gap) {
-				o[0] = 2;
-				put_u32be(o + 1, (uint32_t)prev);
-				put_u32be(o + 5, (uint32_t)gap);
-				if (gap <= 64) {
-					for (uint64_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
-				} else {
-					const uint32_t b = atomicAdd(&n_big, 1u);
-					big_dst[b] = (uint64_t)(o + 9 - out);
-					big_src[b] = prev;
-					big_len[b] = gap;
+		const uint64_t S = scan[255];
+		const uint64_t my = scan[tid] - sz;
+		if (S <= kSerStage) {
+			// ── assemble the tile in LDS ──
+			if (valid) {
+				uint8_t* o = stage + my;
+				if (gap) {
+					o[0] = 2;
+					put_u32be_lds(o + 1, (uint32_t)prev);
+					put_u32be_lds(o + 5, (uint32_t)gap);
+					if (gap <= 64) {
+						for (uint32_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
+					} else {
+						const uint32_t b = atomicAdd(&n_big, 1u);
+						big_dst[b] = (uint32_t)(my + 9);
+						big_src[b] = (uint32_t)prev;
+						big_len[b] = (uint32_t)gap;
+					}
+					o += 9 + gap;
 				}
-				o += 9 + gap;
+				o[0] = 1;
+				put_u32be_lds(o + 1, cr);
+				put_u32be_lds(o + 5, cv);
+				put_u32be_lds(o + 9, cl);
 			}
-			o[0] = 1;
-			put_u32be(o + 1, cr);
-			put_u32be(o + 5, cv);
-			put_u32be(o + 9, cl);
+			__syncthreads();
+			const uint32_t nb = n_big;
+			for (uint32_t b = 0; b < nb; ++b) {
+				uint8_t* d = stage + big_dst[b];
+				const uint8_t* src = V + big_src[b];
+				for (uint32_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
+			}
+			__syncthreads();
+			// ── flush: head bytes to a dword boundary, dwords, tail bytes ──
+			uint8_t* dst = out + pos;
+			const uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
+			const uint32_t Sh = (uint32_t)S;
+			if (tid < head && tid < Sh) dst[tid] = stage[tid];
+			if (Sh > head) {
+				const uint32_t nd = (Sh - head) / 4;
+				uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
+				for (uint32_t k = tid; k < nd; k += 256) {
+					const uint32_t o = head + 4 * k;
+					const uint32_t* w = reinterpret_cast<const uint32_t*>(stage + (o & ~3u));
+					dw[k] = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
+				}
+				const uint32_t tail0 = head + 4 * nd;
+				if (tid < Sh - tail0) dst[tail0 + tid] = stage[tail0 + tid];
+			}
+		} else {
+			// ── direct: each command writes its own bytes ──
+			if (valid) {
+				uint8_t* o = out + pos + my;
+				if (gap) {
+					o[0] = 2;
+					put_u32be(o + 1, (uint32_t)prev);
+					put_u32be(o + 5, (uint32_t)gap);
+					if (gap <= 64) {
+						for (uint64_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
+					} else {
+						const uint32_t b = atomicAdd(&n_big, 1u);
+						big_dst[b] = (uint32_t)(pos + my + 9);
+						big_src[b] = (uint32_t)prev;
+						big_len[b] = (uint32_t)gap;
+					}
+					o += 9 + gap;
+				}
+				o[0] = 1;
+				put_u32be(o + 1, cr);
+				put_u32be(o + 5, cv);
+				put_u32be(o + 9, cl);
+			}
+			__syncthreads();
+			const uint32_t nb = n_big;
+			for (uint32_t b = 0; b < nb; ++b) {
+				uint8_t* d = out + big_dst[b];
+				const uint8_t* src = V + big_src[b];
+				for (uint64_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
+			}
 		}
 		__syncthreads();
-		const uint32_t nb = n_big;
-		for (uint32_t b = 0; b < nb; ++b) {
-			uint8_t* d = out + big_dst[b];
-			const uint8_t* src = V + big_src[b];
-			for (uint64_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
-		}
-		__syncthreads();
-		if (tid == 0) { pos_sh = pos + scan[255]; n_big = 0; }
+		if (tid == 0) { pos_sh = pos + S; n_big = 0; }
 		__syncthreads();
 	}
 

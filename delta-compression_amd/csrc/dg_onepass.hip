@@ -195,6 +195,7 @@ struct GlobalSrc {
 };
 
 constexpr uint32_t kWin = 4096;             // bytes per stream window
+constexpr uint32_t kLook = 32;              // diagonal batch: lookahead bytes per lane
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
@@ -271,7 +272,7 @@ struct WinSrc {
 	// ── diagonal batch ──────────────────────────────────────────────────
 	// State (v0, r0) sits on a mismatch (V[v0] != R[r0]) left by the previous
 	// extension.  Let a_0 = 0 < a_1 < ... be the mismatch offsets along the
-	// diagonal within the next 1 KiB (the end of the shorter stream counts as
+	// diagonal within the next 64 * kLook bytes (the end of the shorter stream counts as
 	// one).  An epoch starting at a_k first sees equal windows at step
 	//   T_k = a_m + 1 - a_k,  m = the first index >= k with a_{m+1} - a_m > p,
 	// and, if it resolves there on the diagonal, emits ADD(T_k bytes) +
@@ -303,19 +304,19 @@ struct WinSrc {
 		*dsz_add = 0;
 		if (lim < p + 1) return 0;
 		[[maybe_unused]] uint64_t tq = PROF_NOW();
-		ensure2(v0, r0, 1024 + 48, true, true);
-		// 1. mismatch bits of offsets [16*lane, 16*lane+16)
-		const uint32_t base = 16 * lane;
+		ensure2(v0, r0, 64 * kLook + 48, true, true);
+		// 1. mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
+		const uint32_t base = kLook * lane;
 		uint32_t bits = 0;
 #pragma unroll
-		for (uint32_t g = 0; g < 4; ++g) {
+		for (uint32_t g = 0; g < kLook / 4; ++g) {
 			const uint32_t x = rd4(0, v0 + base + 4 * g) ^ rd4(1, r0 + base + 4 * g);
 			const uint32_t t = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // byte != 0
 			bits |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * g);
 		}
-		if (base + 16 > lim) {   // past the shorter stream: only its end terminates a match
+		if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
 			bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
-			if (lim >= base && lim < base + 16) bits |= 1u << (lim - base);
+			if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
 		}
 		// 2. ordered list of mismatch offsets (exclusive prefix of counts)
 		const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
@@ -331,31 +332,54 @@ struct WinSrc {
 		tq = PROF_NOW();
 		const uint32_t ak = lane < K ? mlist[lane] : 0xFFFFFFFFu;
 		const uint32_t an = lane + 1 < K ? mlist[lane + 1] : 0xFFFFFFFFu;
-		const uint64_t G = __ballot(lane + 1 < K && an - ak > p);   // a long gap follows a_lane
-		// 3. the chain of epochs (scalar): member j starts at a_cur, first
-		//    equal step T, ends at a_{m+1}; steps laid out from lane B
-		uint32_t cur = 0, B = 0, nm = 0, sumT = 0, maxT = 0;
-		uint64_t starts = 0;
-		uint32_t mstart = 0, mT = 0, mend = 0, mcumT = 0;   // lane j: member j
-		while (nm < 64 && cur + 1 < K) {
-			const uint64_t Gs = G >> cur;
-			if (!Gs) break;
-			const uint32_t m = cur + ffs64(Gs);
-			const uint32_t a0 = rdlane(ak, cur);
-			const uint32_t T = rdlane(ak, m) + 1 - a0;
-			if (T > 63 || B + T + 1 > 64) break;
-			mstart = lane == nm ? a0 : mstart;
-			mT = lane == nm ? T : mT;
-			mend = lane == nm ? rdlane(ak, m + 1) : mend;
-			mcumT = lane == nm ? sumT : mcumT;
-			starts |= 1ull << B;
-			maxT = umax32(maxT, T);
-			B += T + 1;
-			sumT += T;
-			++nm;
-			cur = m + 1;
+		const bool gap = lane + 1 < K && an - ak > p;   // a long gap follows a_lane
+		const uint64_t G = __ballot(gap);
+		// 3. the chain of epochs.  From a_0 the chain visits exactly the
+		//    mismatches that follow a long gap: member r starts right after
+		//    the (r-1)-th long gap and ends (first equal step) at the r-th,
+		//    whose lane k computes it.  Members are laid out over the lanes in
+		//    order, T + 1 steps each, while they fit in 64 lanes and T < 64.
+		const uint64_t gbelow = G & ((1ull << lane) - 1ull);
+		const uint32_t sidx = gbelow ? 64u - (uint32_t)__builtin_clzll(gbelow) : 0u;
+		const uint32_t astart = mlist[sidx];   // sidx <= lane < K
+		const uint32_t T = gap ? ak + 1 - astart : 0u;
+		const uint64_t tooLong = __ballot(gap && T > 63);
+		const uint32_t kb = tooLong ? ffs64(tooLong) : 64u;
+		const uint32_t steps = gap && lane < kb ? T + 1 : 0u;
+		const uint32_t Bend = wave_incl_scan(steps);
+		const bool valid = gap && lane < kb && Bend <= 64;
+		const uint64_t VM = __ballot(valid);
+		if (!VM) return 0;
+		const uint32_t nm = (uint32_t)__builtin_popcountll(VM);
+		const uint32_t klast = 63u - (uint32_t)__builtin_clzll(VM);
+		const uint32_t B = rdlane(Bend, klast);
+		const uint32_t maxT = [&] {
+			uint32_t m = valid ? T : 0u;   // wave max via the same DPP network
+#pragma unroll
+			for (int d = 1; d < 64; d <<= 1) m = umax32(m, (uint32_t)__shfl_xor((int)m, d, 64));
+			return uni(m);
+		}();
+		// member table (LDS, by rank): start | end << 11 | T << 23, and the
+		// step lanes where members begin
+		__builtin_amdgcn_wave_barrier();
+		if (valid) {
+			const uint32_t r = (uint32_t)__builtin_popcountll(gbelow);
+			mlist[64 + r] = astart | (an << 11) | (T << 23);
 		}
-		if (nm == 0) return 0;
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		uint64_t starts = 0;
+		{
+			// flat lane f starts a member iff f == Bend_r - T_r - 1 for a valid r:
+			// mark those lanes through LDS (mlist[0..63] is free again)
+			mlist[lane] = 0u;
+			__builtin_amdgcn_s_waitcnt(0xc07f);
+			__builtin_amdgcn_wave_barrier();
+			if (valid) mlist[Bend - T - 1] = 1u;
+			__builtin_amdgcn_s_waitcnt(0xc07f);
+			__builtin_amdgcn_wave_barrier();
+			starts = __ballot(mlist[lane] != 0u);
+		}
 		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
 		PROF_ADD(*this, P_D_MEMBERS, nm);
 		PROF_ADD(*this, P_D_STEPS, B);
@@ -366,8 +390,9 @@ struct WinSrc {
 		const uint32_t j = live ? (uint32_t)__builtin_popcountll(below) - 1u : 0u;
 		const uint32_t fb = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;   // member's first lane
 		const uint32_t t = lane - fb;
-		const uint32_t js = (uint32_t)__shfl((int)mstart, (int)j, 64);
-		const uint32_t jT = (uint32_t)__shfl((int)mT, (int)j, 64);
+		const uint32_t jw = mlist[64 + (j & 63u)];
+		const uint32_t js = jw & 2047u;
+		const uint32_t jT = jw >> 23;
 		uint32_t sV = kSentinel, sR = kSentinel - 1u, fVl = 0, fRl = 0;
 		PROF_ADD(*this, P_T_D3A, PROF_NOW() - tq);
 		if (live) {
@@ -393,10 +418,12 @@ struct WinSrc {
 					xfv = wave_shr1(xfv);
 					xfr = wave_shr1(xfr);
 				}
-				if (d <= t) {
-					if (xv == sR) { s1 = lane - d; f1 = xfv; }
-					if (xr == sV) { s2 = lane - d; f2 = xfr; }
-				}
+				const bool in = d <= t;
+				const bool m1 = in && xv == sR, m2 = in && xr == sV;
+				s1 = m1 ? lane - d : s1;
+				f1 = m1 ? xfv : f1;
+				s2 = m2 ? lane - d : s2;
+				f2 = m2 ? xfr : f2;
 			}
 		}
 		PROF_ADD(*this, P_T_D3, PROF_NOW() - tq);
@@ -413,18 +440,26 @@ struct WinSrc {
 		}
 		if (t == jT && !hit) bad = true;            // the epoch would go on past T
 		const uint64_t BM = __ballot(live && bad);
-		uint32_t fm = BM ? (uint32_t)__builtin_popcountll(starts & mask_le(ffs64(BM))) - 1u : nm;
+		uint32_t fm = nm, fbad = B;   // committed members, their steps
+		if (BM) {
+			const uint32_t l = ffs64(BM);
+			fbad = 63u - (uint32_t)__builtin_clzll(starts & mask_le(l));   // first lane of its member
+			fm = (uint32_t)__builtin_popcountll(starts & mask_le(l)) - 1u;
+		}
 		if (nrec + fm > rec_cap) fm = 0;
+		if (fm == 0) return 0;
 		// 7. commit members 0 .. fm-1: ADD(T bytes) + COPY(a + T .. end)
 		if (lane < fm) {
+			const uint32_t w = mlist[64 + lane];
+			const uint32_t ms = w & 2047u, me = (w >> 11) & 4095u, mt = w >> 23;
 			uint32_t* o = rec + 3u * (nrec + lane);
-			o[0] = v0 + mstart + mT;
-			o[1] = r0 + mstart + mT;
-			o[2] = mend - mstart - mT;
+			o[0] = v0 + ms + mt;
+			o[1] = r0 + ms + mt;
+			o[2] = me - ms - mt;
 		}
-		const uint32_t cumT = fm < nm ? rdlane(mcumT, fm) : sumT;
-		*dsz_add = 22u * fm + cumT;
-		*adv = fm < nm ? rdlane(mstart, fm) : rdlane(mend, nm - 1);
+		// sum over committed members of (T + 1) is the first lane of member fm
+		*dsz_add = 21u * fm + fbad;
+		*adv = fm < nm ? rdlane(js, fbad) : rdlane(an, klast);
 		*more = fm == nm;
 		PROF_ADD(*this, P_T_D4, PROF_NOW() - tq);
 		return fm;

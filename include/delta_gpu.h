@@ -82,6 +82,9 @@ typedef enum {
 #define DG_OPT_VERBOSE 0
 #define DG_OPT_SPLAY   1
 #define DG_OPT_INPLACE 2
+/* bit index of the in-place cycle policy for DG_OPT_INPLACE encodes
+ * (main.c --policy): clear = localmin, set = constant (delta.h:86) */
+#define DG_OPT_POLICY_CONSTANT 3
 
 /* Layout- and meaning-identical to delta_diff_options_t (src/c/delta.h:248-257):
  * p = seed length, q = hash table size floor (--table-size), buf_cap =
@@ -268,6 +271,28 @@ typedef struct {
 } dg_delta_info_t;
 
 int dg_delta_info(const uint8_t *delta, size_t len, dg_delta_info_t *info);
+
+/* ── in-place conversion (host; src/c/inplace.c:272-736) ───────────────────
+ *
+ * Converts a standard delta against R into an in-place delta: the chain of
+ * main.c `inplace` (main.c:427-480) = delta_decode -> delta_unplace_commands
+ * -> delta_make_inplace(policy) -> delta_encode(inplace = true), byte for
+ * byte.  A delta that is already in-place is returned unchanged
+ * (stats->already_inplace = 1).  Pure host code: no context, no GPU.  The
+ * encoders produce in-place deltas by running this on their output
+ * (dg_encode / dg_encode_batch with DG_OPT_INPLACE, policy from
+ * dg_diff_options_t.flags bit DG_OPT_POLICY_CONSTANT). */
+#define DG_POLICY_LOCALMIN 0
+#define DG_POLICY_CONSTANT 1
+typedef struct {
+	int      already_inplace;
+	uint64_t num_copies, num_adds;
+	uint64_t copy_bytes, add_bytes;
+} dg_inplace_stats_t;
+
+int dg_make_inplace(const uint8_t *r, size_t r_len, const uint8_t *delta,
+                    size_t delta_len, int policy, dg_buffer_t *out,
+                    dg_inplace_stats_t *stats);
 
 /* ── synthetic batch generators (bench / test inputs, on the device) ─────
  * Workload definitions in DESIGN.md ("Synthetic inputs"); the oracle's

@@ -310,3 +310,43 @@ def test_decode_plan_batch_mixed(dg, ctx, orc, torch_cuda):
             if want == 0:
                 assert lc[i] == len(V)
                 assert bytes(oc[ds[4]:ds[4] + len(V)].numpy()) == V, i
+
+
+def test_encode_inplace_vs_reference_golden(dg, ctx, orc):
+    """dg_encode with DG_OPT_INPLACE (device encode + host CRWI conversion)
+    reproduces every reference in-place delta (main.c encode --inplace)."""
+    import json
+    from test_oracle import inplace_inputs
+    here = os.path.dirname(os.path.abspath(__file__))
+    pol = {0: "localmin", 1: "constant"}
+    for c in json.load(open(os.path.join(here, "golden", "golden_inplace.json")))["cases"]:
+        R, V = inplace_inputs(orc, c)
+        algo = "onepass" if c["algo"] == ONEPASS else "correcting"
+        got = dg.encode(R, V, algo, p=16, q=c["q"], inplace=True, policy=pol[c["policy"]], ctx=ctx)
+        assert got == bytes.fromhex(c["delta_hex"]), c["name"]
+
+
+def test_cli_encode_inplace_vs_reference(tmp_path, orc):
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    cli = os.path.join(os.path.dirname(here), "delta-compression_amd", "bin", "delta")
+    ref_cli = os.path.join(os.path.dirname(here), "oracle", "_ref", "delta")
+    R, V = orc.synth_transpose(0xC4000001, 9, 4000, 50)
+    (tmp_path / "r").write_bytes(R)
+    (tmp_path / "v").write_bytes(V)
+    for pol in ([], ["--policy", "constant"]):
+        args = ["encode", "correcting", str(tmp_path / "r"), str(tmp_path / "v")]
+        a = subprocess.run([cli] + args + [str(tmp_path / "d"), "--inplace", "--table-size", "1"] + pol,
+                           capture_output=True, text=True)
+        assert a.returncode == 0, a.stderr
+        d = (tmp_path / "d").read_bytes()
+        assert d[4] == 1
+        c = subprocess.run([cli, "decode", str(tmp_path / "r"), str(tmp_path / "d"), str(tmp_path / "o")],
+                           capture_output=True, text=True)
+        assert c.returncode == 0 and (tmp_path / "o").read_bytes() == V
+        if os.path.exists(ref_cli):
+            b = subprocess.run([ref_cli] + args + [str(tmp_path / "d_ref"), "--inplace", "--table-size", "1"]
+                               + pol, capture_output=True, text=True)
+            assert (tmp_path / "d_ref").read_bytes() == d
+            strip = lambda s: [l for l in s.splitlines() if not l.startswith(("Time:", "Delta:"))]
+            assert strip(a.stdout) == strip(b.stdout)
