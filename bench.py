@@ -61,6 +61,22 @@ def load_product():
     return mod
 
 
+def pmc_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (scripts/pmc_traffic.sh -> profiles/<round>_pmc_traffic_<config>.json:
+    FETCH_SIZE/WRITE_SIZE passes, gfx950 corrections applied), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{config}.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("kernel") == kernel and d.get("hbm_bytes_per_launch"):
+            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(cfg, n_pairs_sample, threads):
     """The reference's src/c (oracle/_ref/ref_bench, compiled from
     /root/reference by oracle/Makefile) on the host cores, bounded sample of
@@ -283,6 +299,10 @@ def main():
     avg_diff_s = diff_ms / args.steps / 1e3
     achieved = in_bytes_rank / avg_diff_s / 1e9 if avg_diff_s > 0 else 0.0
     delta_bytes = int(offs[-1].item())
+    kname = ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
+             else "onepass16_kernel" if plan_aligned16 else "onepass_kernel")
+    traffic, traffic_src = pmc_traffic(args.config, kname) if npg == CONFIGS[args.config][0] \
+        else (None, None)
 
     if rank == 0:
         line = {
@@ -316,13 +336,13 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
-                           else "onepass16_kernel" if plan_aligned16 else "onepass_kernel"),
+                "kernel": kname,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": in_bytes_rank,
                 "avg_launch_ms": round(avg_diff_s * 1e3, 4),
                 "crc_ms_per_step": round(crc_ms / args.steps, 4),
