@@ -102,6 +102,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 	return x;
 }
 
+// inclusive prefix max over the wave (same DPP network as wave_incl_scan)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+	return x;
+}
+
 __device__ __forceinline__ uint64_t quad_sum64(uint64_t x) {
 	uint64_t y = ((uint64_t)dpp_xor1((uint32_t)(x >> 32)) << 32) | dpp_xor1((uint32_t)x);
 	x += y;
@@ -345,124 +356,129 @@ struct WinSrc {
 		const uint32_t T = gap ? ak + 1 - astart : 0u;
 		const uint64_t tooLong = __ballot(gap && T > 63);
 		const uint32_t kb = tooLong ? ffs64(tooLong) : 64u;
-		const uint32_t steps = gap && lane < kb ? T + 1 : 0u;
-		const uint32_t Bend = wave_incl_scan(steps);
-		const bool valid = gap && lane < kb && Bend <= 64;
-		const uint64_t VM = __ballot(valid);
-		if (!VM) return 0;
-		const uint32_t nm = (uint32_t)__builtin_popcountll(VM);
-		const uint32_t klast = 63u - (uint32_t)__builtin_clzll(VM);
-		const uint32_t B = rdlane(Bend, klast);
-		const uint32_t maxT = [&] {
-			uint32_t m = valid ? T : 0u;   // wave max via the same DPP network
-#pragma unroll
-			for (int d = 1; d < 64; d <<= 1) m = umax32(m, (uint32_t)__shfl_xor((int)m, d, 64));
-			return uni(m);
-		}();
-		// member table (LDS, by rank): start | end << 11 | T << 23, and the
-		// step lanes where members begin
-		__builtin_amdgcn_wave_barrier();
-		if (valid) {
-			const uint32_t r = (uint32_t)__builtin_popcountll(gbelow);
-			mlist[64 + r] = astart | (an << 11) | (T << 23);
-		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		uint64_t starts = 0;
-		{
-			// flat lane f starts a member iff f == Bend_r - T_r - 1 for a valid r:
-			// mark those lanes through LDS (mlist[0..63] is free again)
+		const bool cand = gap && lane < kb;        // members, in chain order
+		const uint32_t Bend = wave_incl_scan(cand ? T + 1 : 0u);   // steps through this member
+		uint64_t left = __ballot(cand);
+		if (!left) return 0;
+		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
+		// Members are taken in rounds of at most 64 steps (a member never
+		// straddles two rounds); the first member that fails its check ends
+		// the batch.
+		uint32_t committed = 0, dadd = 0, rbase = 0, advance = 0;
+		bool all = true;
+		while (left) {
+			tq = PROF_NOW();
+			const bool valid = ((left >> lane) & 1u) && Bend - rbase <= 64;
+			const uint64_t VM = __ballot(valid);
+			const uint32_t nm = (uint32_t)__builtin_popcountll(VM);
+			const uint32_t klast = 63u - (uint32_t)__builtin_clzll(VM);
+			const uint32_t B = rdlane(Bend, klast) - rbase;
+			const uint32_t maxT = rdlane(wave_incl_max(valid ? T : 0u), 63);
+			// member table (LDS, by rank in the round): start | end << 11 |
+			// T << 23, and the step lanes where members begin
+			__builtin_amdgcn_wave_barrier();
+			if (valid) {
+				const uint32_t r = (uint32_t)__builtin_popcountll(VM & ((1ull << lane) - 1ull));
+				mlist[64 + r] = astart | (an << 11) | (T << 23);
+			}
 			mlist[lane] = 0u;
 			__builtin_amdgcn_s_waitcnt(0xc07f);
 			__builtin_amdgcn_wave_barrier();
-			if (valid) mlist[Bend - T - 1] = 1u;
+			if (valid) mlist[Bend - rbase - T - 1] = 1u;
 			__builtin_amdgcn_s_waitcnt(0xc07f);
 			__builtin_amdgcn_wave_barrier();
-			starts = __ballot(mlist[lane] != 0u);
-		}
-		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
-		PROF_ADD(*this, P_D_MEMBERS, nm);
-		PROF_ADD(*this, P_D_STEPS, B);
-		tq = PROF_NOW();
-		// 4. windows of every step: lane f is step t of member j
-		const bool live = lane < B;
-		const uint64_t below = starts & mask_le(lane);
-		const uint32_t j = live ? (uint32_t)__builtin_popcountll(below) - 1u : 0u;
-		const uint32_t fb = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;   // member's first lane
-		const uint32_t t = lane - fb;
-		const uint32_t jw = mlist[64 + (j & 63u)];
-		const uint32_t js = jw & 2047u;
-		const uint32_t jT = jw >> 23;
-		uint32_t sV = kSentinel, sR = kSentinel - 1u, fVl = 0, fRl = 0;
-		PROF_ADD(*this, P_T_D3A, PROF_NOW() - tq);
-		if (live) {
-			const uint64_t fV = fp16(0, v0 + js + t), fR = fp16(1, r0 + js + t);
-			sV = (uint32_t)mod_q(fV, q, qmag);
-			sR = (uint32_t)mod_q(fR, q, qmag);
-			fVl = (uint32_t)fV;
-			fRl = (uint32_t)fR;
-		}
-		// 5. first writers: s1 = first lane c in [fb, lane] with sV(c) == sR(lane),
-		//    s2 = first with sR(c) == sV(lane)
-		PROF_ADD(*this, P_T_D3B, PROF_NOW() - tq);
-		//    Lane l looks back d = 0 .. t lanes (its own member's earlier
-		//    steps) through DPP wave shifts; the largest matching d is the
-		//    earliest writer, whose fingerprint rides along.
-		uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
-		{
-			uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
-			for (uint32_t d = 0; d <= maxT; ++d) {
-				if (d) {
-					xv = wave_shr1(xv);
-					xr = wave_shr1(xr);
-					xfv = wave_shr1(xfv);
-					xfr = wave_shr1(xfr);
-				}
-				const bool in = d <= t;
-				const bool m1 = in && xv == sR, m2 = in && xr == sV;
-				s1 = m1 ? lane - d : s1;
-				f1 = m1 ? xfv : f1;
-				s2 = m2 ? lane - d : s2;
-				f2 = m2 ? xfr : f2;
+			const uint64_t starts = __ballot(mlist[lane] != 0u);
+			PROF_ADD(*this, P_D_MEMBERS, nm);
+			PROF_ADD(*this, P_D_STEPS, B);
+			// 4. windows of every step: lane f is step t of member j
+			const bool live = lane < B;
+			const uint64_t below = starts & mask_le(lane);
+			const uint32_t j = live ? (uint32_t)__builtin_popcountll(below) - 1u : 0u;
+			const uint32_t fb = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;   // member's first lane
+			const uint32_t t = lane - fb;
+			const uint32_t jw = mlist[64 + (j & 63u)];
+			const uint32_t js = jw & 2047u;
+			const uint32_t jT = jw >> 23;
+			uint32_t sV = kSentinel, sR = kSentinel - 1u, fVl = 0, fRl = 0;
+			PROF_ADD(*this, P_T_D3A, PROF_NOW() - tq);
+			if (live) {
+				const uint64_t fV = fp16(0, v0 + js + t), fR = fp16(1, r0 + js + t);
+				sV = (uint32_t)mod_q(fV, q, qmag);
+				sR = (uint32_t)mod_q(fR, q, qmag);
+				fVl = (uint32_t)fV;
+				fRl = (uint32_t)fR;
 			}
+			PROF_ADD(*this, P_T_D3B, PROF_NOW() - tq);
+			// 5. first writers: s1 = first lane c in [fb, lane] with sV(c) ==
+			//    sR(lane), s2 = first with sR(c) == sV(lane).  Lane l looks back
+			//    d = 0 .. t lanes (its own member's earlier steps) through DPP
+			//    wave shifts; the largest matching d is the earliest writer,
+			//    whose fingerprint rides along.
+			uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
+			{
+				uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
+				for (uint32_t d = 0; d <= maxT; ++d) {
+					if (d) {
+						xv = wave_shr1(xv);
+						xr = wave_shr1(xr);
+						xfv = wave_shr1(xfv);
+						xfr = wave_shr1(xfr);
+					}
+					const bool in = d <= t;
+					const bool m1 = in && xv == sR, m2 = in && xr == sV;
+					s1 = m1 ? lane - d : s1;
+					f1 = m1 ? xfv : f1;
+					s2 = m2 ? lane - d : s2;
+					f2 = m2 ? xfr : f2;
+				}
+			}
+			PROF_ADD(*this, P_T_D3, PROF_NOW() - tq);
+			tq = PROF_NOW();
+			// 6. the reference's resolution of step t
+			bool bad = false, hit = false;
+			if (s1 != 64) {
+				if (s1 == lane) hit = t == jT;          // the diagonal: equal bytes iff t == T
+				else if (f1 == fRl) bad = true;         // a possible match off the diagonal
+			}
+			if (!hit && !bad && s2 != 64) {
+				if (s2 == lane) hit = t == jT;
+				else if (f2 == fVl) bad = true;
+			}
+			if (t == jT && !hit) bad = true;            // the epoch would go on past T
+			const uint64_t BM = __ballot(live && bad);
+			uint32_t fm = nm, fbad = B;   // committed members, their steps
+			if (BM) {
+				const uint32_t l = ffs64(BM);
+				fbad = 63u - (uint32_t)__builtin_clzll(starts & mask_le(l));   // first lane of its member
+				fm = (uint32_t)__builtin_popcountll(starts & mask_le(l)) - 1u;
+			}
+			if (nrec + committed + fm > rec_cap) { fm = 0; fbad = 0; }
+			// 7. commit members 0 .. fm-1: ADD(T bytes) + COPY(a + T .. end)
+			if (lane < fm) {
+				const uint32_t w = mlist[64 + lane];
+				const uint32_t ms = w & 2047u, me = (w >> 11) & 4095u, mt = w >> 23;
+				uint32_t* o = rec + 3u * (nrec + committed + lane);
+				o[0] = v0 + ms + mt;
+				o[1] = r0 + ms + mt;
+				o[2] = me - ms - mt;
+			}
+			// sum over committed members of (T + 1) is the first lane of member fm
+			dadd += 21u * fm + fbad;
+			committed += fm;
+			PROF_ADD(*this, P_T_D4, PROF_NOW() - tq);
+			if (fm < nm) {   // stop at the failing member's start
+				advance = rdlane(js, fbad);
+				all = false;
+				break;
+			}
+			advance = rdlane(an, klast);
+			rbase = rdlane(Bend, klast);
+			left &= ~VM;
 		}
-		PROF_ADD(*this, P_T_D3, PROF_NOW() - tq);
-		tq = PROF_NOW();
-		// 6. the reference's resolution of step t
-		bool bad = false, hit = false;
-		if (s1 != 64) {
-			if (s1 == lane) hit = t == jT;          // the diagonal: equal bytes iff t == T
-			else if (f1 == fRl) bad = true;         // a possible match off the diagonal
-		}
-		if (!hit && !bad && s2 != 64) {
-			if (s2 == lane) hit = t == jT;
-			else if (f2 == fVl) bad = true;
-		}
-		if (t == jT && !hit) bad = true;            // the epoch would go on past T
-		const uint64_t BM = __ballot(live && bad);
-		uint32_t fm = nm, fbad = B;   // committed members, their steps
-		if (BM) {
-			const uint32_t l = ffs64(BM);
-			fbad = 63u - (uint32_t)__builtin_clzll(starts & mask_le(l));   // first lane of its member
-			fm = (uint32_t)__builtin_popcountll(starts & mask_le(l)) - 1u;
-		}
-		if (nrec + fm > rec_cap) fm = 0;
-		if (fm == 0) return 0;
-		// 7. commit members 0 .. fm-1: ADD(T bytes) + COPY(a + T .. end)
-		if (lane < fm) {
-			const uint32_t w = mlist[64 + lane];
-			const uint32_t ms = w & 2047u, me = (w >> 11) & 4095u, mt = w >> 23;
-			uint32_t* o = rec + 3u * (nrec + lane);
-			o[0] = v0 + ms + mt;
-			o[1] = r0 + ms + mt;
-			o[2] = me - ms - mt;
-		}
-		// sum over committed members of (T + 1) is the first lane of member fm
-		*dsz_add = 21u * fm + fbad;
-		*adv = fm < nm ? rdlane(js, fbad) : rdlane(an, klast);
-		*more = fm == nm;
-		PROF_ADD(*this, P_T_D4, PROF_NOW() - tq);
-		return fm;
+		*adv = advance;
+		*dsz_add = dadd;
+		*more = all;
+		return committed;
 	}
 
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
