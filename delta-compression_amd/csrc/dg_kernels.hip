@@ -284,10 +284,19 @@ __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
 	return up & ~dn;
 }
 
-__global__ __launch_bounds__(256) void crc_segments_kernel(CrcArgs a) {
-	__shared__ uint64_t T[8 * 256 + kCrcLevels * kCrcNibTabWords];
-	for (uint32_t i = threadIdx.x; i < 8 * 256 + kCrcLevels * kCrcNibTabWords; i += 256)
-		T[i] = a.tables[i];
+// slicing-by-4 step: the register's low 32 bits absorb one little-endian word
+__device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint64_t* __restrict__ T) {
+	const uint64_t x = crc ^ w;
+	return T[3 * 256 + (x & 0xff)] ^ T[2 * 256 + ((x >> 8) & 0xff)] ^ T[256 + ((x >> 16) & 0xff)] ^
+	       T[(x >> 24) & 0xff] ^ (x >> 32);
+}
+
+// Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
+// and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
+// tables read through the cache, at most 64 VGPRs.
+__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
+	__shared__ uint64_t T[4 * 256];
+	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
 	__syncthreads();
 	const uint32_t wave = threadIdx.x >> 6;
 	const uint32_t lane = lane_id();
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(256) void crc_segments_kernel(CrcArgs a) {
 	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
 
 	uint64_t reg = 0;
-	constexpr int kPf = 8;   // 16-byte loads in flight per lane
+	constexpr int kPf = 4;   // 16-byte loads in flight per lane
 	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
 		ulonglong2 xs[kPf];
 #pragma unroll
@@ -328,12 +337,14 @@ __global__ __launch_bounds__(256) void crc_segments_kernel(CrcArgs a) {
 				lo ^= byte_mask(fc, fc + 8);
 				hi ^= byte_mask(fc - 8, fc);
 			}
-			reg = slice8(reg ^ lo, T);
-			reg = slice8(reg ^ hi, T);
+			reg = slice4(reg, (uint32_t)lo, T);
+			reg = slice4(reg, (uint32_t)(lo >> 32), T);
+			reg = slice4(reg, (uint32_t)hi, T);
+			reg = slice4(reg, (uint32_t)(hi >> 32), T);
 		}
 	}
 	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
-	const uint64_t* L = T + 8 * 256;
+	const uint64_t* L = a.tables + 8 * 256;
 #pragma unroll
 	for (int lv = 0; lv < kCrcLevels; ++lv) {
 		const int d = 1 << lv;

@@ -207,6 +207,7 @@ struct GlobalSrc {
 
 constexpr uint32_t kWin = 4096;             // bytes per stream window
 constexpr uint32_t kLook = 32;              // diagonal batch: lookahead bytes per lane
+constexpr uint32_t kShortT = 12;            // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
@@ -415,7 +416,7 @@ struct WinSrc {
 			//    wave shifts; the largest matching d is the earliest writer,
 			//    whose fingerprint rides along.
 			uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
-			{
+			if (maxT <= kShortT) {
 				uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
 				for (uint32_t d = 0; d <= maxT; ++d) {
 					if (d) {
@@ -430,6 +431,49 @@ struct WinSrc {
 					f1 = m1 ? xfv : f1;
 					s2 = m2 ? lane - d : s2;
 					f2 = m2 ? xfr : f2;
+				}
+			} else {
+				// Long epochs: a 2048-bit hash of the round's V slots and of
+				// its R slots (LDS) flags the steps that can have a candidate
+				// at all (every epoch's last step is among them); only those
+				// are resolved exactly, one ballot per lookup.
+				uint32_t* bmv = mlist + 128;
+				uint32_t* bmr = mlist + 192;
+				__builtin_amdgcn_wave_barrier();
+				bmv[lane] = 0u;
+				bmr[lane] = 0u;
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+				if (live) {
+					atomicOr(&bmv[(sV >> 5) & 63u], 1u << (sV & 31u));
+					atomicOr(&bmr[(sR >> 5) & 63u], 1u << (sR & 31u));
+				}
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+				const bool q1 = live && ((bmv[(sR >> 5) & 63u] >> (sR & 31u)) & 1u);
+				const bool q2 = live && ((bmr[(sV >> 5) & 63u] >> (sV & 31u)) & 1u);
+				const uint64_t Q1 = __ballot(q1), Q2 = __ballot(q2);
+				for (uint64_t w = Q1 | Q2; w; w &= w - 1) {
+					const uint32_t L = ffs64(w);
+					const uint64_t range = mask_le(L) & ~((1ull << rdlane(fb, L)) - 1ull);   // [fb_L, L]
+					if ((Q1 >> L) & 1u) {
+						const uint64_t m = __ballot(sV == rdlane(sR, L)) & range;
+						if (m) {
+							const uint32_t c = ffs64(m);
+							const uint32_t fc = rdlane(fVl, c);
+							s1 = lane == L ? c : s1;
+							f1 = lane == L ? fc : f1;
+						}
+					}
+					if ((Q2 >> L) & 1u) {
+						const uint64_t m = __ballot(sR == rdlane(sV, L)) & range;
+						if (m) {
+							const uint32_t c = ffs64(m);
+							const uint32_t fc = rdlane(fRl, c);
+							s2 = lane == L ? c : s2;
+							f2 = lane == L ? fc : f2;
+						}
+					}
 				}
 			}
 			PROF_ADD(*this, P_T_D3, PROF_NOW() - tq);
@@ -787,7 +831,7 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
 __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
-	__shared__ uint32_t bm[128];
+	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch list, member table, round bitmaps
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
