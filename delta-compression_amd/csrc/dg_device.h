@@ -72,6 +72,12 @@ struct EncodeArgs {
 	uint32_t n_tables;
 	uint32_t* table_locks;
 	uint32_t* table_tags;
+	// fused serialisation (onepass16_kernel): packed output, offsets and the
+	// per-pair look-back words; lookback == nullptr selects scan + serialise
+	uint8_t* out;
+	uint64_t out_cap;
+	uint64_t* offsets;
+	unsigned long long* lookback;
 	// correcting
 	uint32_t buf_cap;          // lookback buffer entries (correcting.c:14-62)
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
@@ -132,9 +138,12 @@ struct SynthCopy {   // V[dst..+len) = R[src..+len)
 // launchers (dg_kernels.hip)
 #ifdef __HIP_PLATFORM_AMD__
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
+bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);
+hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
+                            const int32_t* status, uint32_t n, hipStream_t st);
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,

@@ -296,12 +296,14 @@ struct dg_encode_plan {
 	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
-	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab;
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
+	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
+	bool fused = false;        // onepass16 serialises in-kernel (DG_UNFUSED=1: scan + serialise)
 	// timing
 	bool timing = false;
 	// timing: `slots` sets of kTimingEvents events, one set per run (ring)
@@ -451,6 +453,12 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_locks.alloc(4ull * P->n_tables);
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
 	if (algo == DG_ALGO_CORRECTING) bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
+	{
+		const char* uf = getenv("DG_UNFUSED");
+		P->fused = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
+		           !(uf && uf[0] == '1');
+	}
+	if (P->fused) bad |= P->d_lookback.alloc(8ull * std::max<uint32_t>(n, 1));
 	if (bad) {
 		delete P;
 		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
@@ -474,6 +482,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	}
 	const char* sc = getenv("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
+	const char* cf = getenv("DG_CRC_FIRST");
+	P->crc_first = cf && cf[0] == '1';
 	if (!P->serial_crc) {
 		e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
 		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
@@ -600,6 +610,13 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)P->opts.buf_cap;
 		if (P->algo == DG_ALGO_ONEPASS) {
+			if (P->fused) {
+				a.out = d_out;
+				a.out_cap = out_cap;
+				a.offsets = d_offsets;
+				a.lookback = P->d_lookback.as<unsigned long long>();
+				HIPCHK(ctx, hipMemsetAsync(P->d_lookback.p, 0, 8ull * P->n, st));
+			}
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 		} else {
 			// fresh R indexes (~0 = empty slot), then build + scan
@@ -618,9 +635,23 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	} else {
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
-		if ((rc = run_diff()) != DG_OK) return rc;
-		if ((rc = run_crc()) != DG_OK) return rc;
+		if (P->crc_first) {   // A/B: CRC waves dispatched first
+			if ((rc = run_crc()) != DG_OK) return rc;
+			if ((rc = run_diff()) != DG_OK) return rc;
+		} else {
+			if ((rc = run_diff()) != DG_OK) return rc;
+			if ((rc = run_crc()) != DG_OK) return rc;
+		}
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
+	}
+	if (P->fused) {
+		// the differencing kernel placed and serialised every delta; only the
+		// header CRCs remain, once the CRC stream has joined
+		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
+		HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
+		return DG_OK;
 	}
 	// 3. exclusive scan of sizes -> packed offsets
 	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));

@@ -458,6 +458,27 @@ hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* s
 	return hipGetLastError();
 }
 
+// header bytes 9..24 (src/dst CRC, big-endian, encoding.c:52-54) of deltas
+// serialised before their CRCs were known
+__global__ __launch_bounds__(256) void crc_patch_kernel(uint8_t* out, const uint64_t* offsets,
+                                                        const uint64_t* crc, const int32_t* status,
+                                                        uint32_t n) {
+	const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+	if (i >= n || status[i] != 0) return;
+	uint8_t* h = out + offsets[i];
+	const uint64_t cs = crc[2ull * i], cd = crc[2ull * i + 1];
+	for (int k = 0; k < 8; ++k) {
+		h[9 + k] = (uint8_t)(cs >> (56 - 8 * k));
+		h[17 + k] = (uint8_t)(cd >> (56 - 8 * k));
+	}
+}
+
+hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
+                            const int32_t* status, uint32_t n, hipStream_t st) {
+	if (n) hipLaunchKernelGGL(crc_patch_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, offsets, crc, status, n);
+	return hipGetLastError();
+}
+
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
 	return hipGetLastError();

@@ -47,6 +47,7 @@
 
 #include "dg_device.h"
 #include "dg_devutil.h"
+#include "dg_serialize_wave.h"
 
 namespace dg {
 
@@ -552,8 +553,14 @@ struct WinSrc {
 
 // ───────────────────────────── the epoch chain ────────────────────────────
 
+struct PairResult {
+	uint32_t nrec;
+	uint64_t dsz;
+	int32_t st;
+};
+
 template <class Src>
-__device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
+__device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
                                              const uint64_t (&cA)[4], uint32_t* bm) {
 	const uint32_t lane = lane_id();
@@ -826,6 +833,7 @@ __device__ __forceinline__ void onepass_pair(Src& src, const EncodeArgs& a, uint
 			for (int i = 0; i < kProfN; ++i) atomicAdd(&g_onepass_prof[i], (unsigned long long)src.prof[i]);
 	}
 #endif
+	return PairResult{nrec, dsz, st};
 }
 
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
@@ -850,7 +858,25 @@ __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	const uint32_t part = lane_id() & 3u;
 #pragma unroll
 	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
-	onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+	if (a.lookback) {
+		// fused placement + serialisation (dg_serialize_wave.h)
+		const uint64_t off = lookback_offset(a.lookback, pair, res.dsz);
+		const uint32_t lane = lane_id();
+		if (lane == 0) {
+			a.offsets[pair] = off;
+			if (pair + 1 == a.n_pairs) a.offsets[a.n_pairs] = off + res.dsz;
+		}
+		int32_t st = uni((uint32_t)res.st);
+		if (st == 0 && off + res.dsz > a.out_cap) st = 7;
+		if (st == 0) {
+			vm_drain();   // this wave's record stores have landed
+			__builtin_amdgcn_s_waitcnt(0xc07f);
+			st = serialize_wave<2 * kWinStride - 32>(a.out + off, res.dsz, a.ver + pd.v_off, (uint32_t)pd.v_len,
+			                                         a.rec + 3ull * pp.rec_base, res.nrec, (sw_lds8*)win);
+		}
+		if (lane == 0 && st != res.st) a.status[pair] = st;
+	}
 #ifdef DG_ONEPASS_PROF
 	if (lane_id() == 0) atomicAdd(&g_onepass_prof[P_T_TOTAL], (unsigned long long)(PROF_NOW() - t_start));
 #endif
@@ -875,10 +901,14 @@ static bool force_global_src() {
 	return e && e[0] == '1';
 }
 
+bool onepass16_selected() { return !force_global_src(); }
+
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
 	if (a.n_pairs == 0) return hipSuccess;
 	if (p == 16 && aligned16 && !force_global_src())
 		hipLaunchKernelGGL(onepass16_kernel, dim3(a.n_pairs), dim3(64), 0, st, a);
+	else if (a.lookback)
+		return hipErrorInvalidValue;   // fused serialisation needs onepass16_kernel
 	else if (p == 16)
 		hipLaunchKernelGGL(onepass_kernel<16>, dim3(a.n_pairs), dim3(64), 0, st, a);
 	else
