@@ -82,6 +82,7 @@ struct EncodeArgs {
 	uint32_t buf_cap;          // lookback buffer entries (correcting.c:14-62)
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
+	uint32_t wave_prio;        // onepass16: s_setprio level (issue priority over the CRC waves)
 };
 
 struct SerArgs {

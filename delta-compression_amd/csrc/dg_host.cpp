@@ -303,7 +303,8 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
-	bool fused = false;        // onepass16 serialises in-kernel (DG_UNFUSED=1: scan + serialise)
+	uint32_t wave_prio = 0;    // DG_WAVE_PRIO: onepass16 s_setprio level
+	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
 	bool timing = false;
 	// timing: `slots` sets of kTimingEvents events, one set per run (ring)
@@ -454,9 +455,12 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
 	if (algo == DG_ALGO_CORRECTING) bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
 	{
-		const char* uf = getenv("DG_UNFUSED");
+		// DG_FUSED=1: onepass16 serialises in-kernel behind a decoupled look-back.
+		// Off by default: the look-back couples every wave to the slowest pair
+		// before it, which cost 20-25% at C2/C3 on MI355X (profiles/r01_ab_fused_vs_unfused.txt).
+		const char* fz = getenv("DG_FUSED");
 		P->fused = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
-		           !(uf && uf[0] == '1');
+		           fz && fz[0] == '1';
 	}
 	if (P->fused) bad |= P->d_lookback.alloc(8ull * std::max<uint32_t>(n, 1));
 	if (bad) {
@@ -482,6 +486,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	}
 	const char* sc = getenv("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
+	const char* wp = getenv("DG_WAVE_PRIO");
+	P->wave_prio = wp ? (uint32_t)atoi(wp) : 0;
 	const char* cf = getenv("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
 	if (!P->serial_crc) {
@@ -609,6 +615,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_locks = P->d_locks.as<uint32_t>();
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)P->opts.buf_cap;
+		a.wave_prio = P->wave_prio;
 		if (P->algo == DG_ALGO_ONEPASS) {
 			if (P->fused) {
 				a.out = d_out;

@@ -842,6 +842,9 @@ __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch list, member table, round bitmaps
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
+	if (a.wave_prio == 1) __builtin_amdgcn_s_setprio(1);
+	else if (a.wave_prio == 2) __builtin_amdgcn_s_setprio(2);
+	else if (a.wave_prio >= 3) __builtin_amdgcn_s_setprio(3);
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	WinSrc src;

@@ -7,7 +7,7 @@ TAG=${1:-x}
 O=gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -q -m gpu -x > $O/$TAG.tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/$TAG.tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread >$O/$TAG.tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/$TAG.tests.log; exit 1; }
 tail -2 $O/$TAG.tests.log
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/$TAG.c2.json 2> $O/$TAG.c2.err || { echo "bench c2 rc=$?"; tail $O/$TAG.c2.err; exit 1; }
 cat $O/$TAG.c2.json
