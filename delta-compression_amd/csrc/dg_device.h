@@ -54,6 +54,7 @@ struct CrcSpanDev {
 constexpr int kCrcLevels = 6;          // in-wave tree levels
 constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
 
+
 struct EncodeArgs {
 	const uint8_t* ref;
 	const uint8_t* ver;
@@ -83,6 +84,7 @@ struct EncodeArgs {
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
 	uint32_t wave_prio;        // onepass16: s_setprio level (issue priority over the CRC waves)
+	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
 };
 
 struct SerArgs {

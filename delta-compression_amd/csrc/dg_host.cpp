@@ -304,6 +304,7 @@ struct dg_encode_plan {
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	uint32_t wave_prio = 0;    // DG_WAVE_PRIO: onepass16 s_setprio level
+	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
 	bool timing = false;
@@ -488,6 +489,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->serial_crc = sc && sc[0] == '1';
 	const char* wp = getenv("DG_WAVE_PRIO");
 	P->wave_prio = wp ? (uint32_t)atoi(wp) : 0;
+	const char* db = getenv("DG_DEBUG_BITS");
+	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = getenv("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
 	if (!P->serial_crc) {
@@ -616,6 +619,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)P->opts.buf_cap;
 		a.wave_prio = P->wave_prio;
+		a.dbg = P->dbg;
 		if (P->algo == DG_ALGO_ONEPASS) {
 			if (P->fused) {
 				a.out = d_out;

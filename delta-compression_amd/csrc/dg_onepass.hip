@@ -862,6 +862,7 @@ __global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
 #pragma unroll
 	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
 	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
 	if (a.lookback) {
 		// fused placement + serialisation (dg_serialize_wave.h)
 		const uint64_t off = lookback_offset(a.lookback, pair, res.dsz);
