@@ -18,7 +18,7 @@ constexpr uint32_t kCrcWavesPerBlock = 4;
 
 // Onepass register history: chunks of 64 steps kept in VGPRs before the
 // epoch spills into a global (slot, tag) table.
-constexpr int kHistChunks = 8;
+constexpr int kHistChunks = 4;   // 94 VGPRs: 5 waves/SIMD (8 chunks: 113 VGPRs, 4 waves)
 
 struct PairDev {          // == dg_pair_t
 	uint64_t r_off, r_len, v_off, v_len;
@@ -144,7 +144,8 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
-hipError_t launch_serialize(const SerArgs& s, hipStream_t st);
+hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs
+hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st);

@@ -305,6 +305,7 @@ struct dg_encode_plan {
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	uint32_t wave_prio = 0;    // DG_WAVE_PRIO: onepass16 s_setprio level
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches
+	bool ser_block = false;    // DG_SER_BLOCK=1: block-per-pair serialiser (A/B)
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
 	bool timing = false;
@@ -314,7 +315,7 @@ struct dg_encode_plan {
 	hipEvent_t* cur = nullptr;   // event set of the run being enqueued
 };
 
-static const char* kStageNames[] = {"crc64", "diff", "scan+join", "serialize", "total"};
+static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total"};
 
 extern "C" {
 
@@ -487,6 +488,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	}
 	const char* sc = getenv("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
+	const char* sb = getenv("DG_SER_BLOCK");
+	P->ser_block = sb && sb[0] == '1';
 	const char* wp = getenv("DG_WAVE_PRIO");
 	P->wave_prio = wp ? (uint32_t)atoi(wp) : 0;
 	const char* db = getenv("DG_DEBUG_BITS");
@@ -536,7 +539,8 @@ int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 }
 
 // Per-run events: 0/1 around the CRC kernels (side stream), 2/3 around the
-// differencing kernel, 4 after the scan + CRC join, 5 after serialisation.
+// differencing kernel, 4 after the scan, 5 after serialisation + the CRC join
+// + the header patch (DG_SER_BLOCK=1 / DG_FUSED=1: the join falls before 4).
 // Returns the mean over the runs recorded since set_timing (at most `slots`).
 int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
 	if (!P || !P->slots || !P->runs) return 0;
@@ -666,24 +670,32 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	}
 	// 3. exclusive scan of sizes -> packed offsets
 	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
-	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
-	// 4. serialise
-	{
-		SerArgs s{};
-		s.ver = d_ver;
-		s.pairs = P->d_pairs.as<PairDev>();
-		s.pplan = P->d_pplan.as<PairPlanDev>();
-		s.rec = P->d_rec.as<uint32_t>();
-		s.n_rec = P->d_nrec.as<uint32_t>();
-		s.crc = P->d_crc.as<uint64_t>();
-		s.offsets = d_offsets;
-		s.out = d_out;
-		s.out_cap = out_cap;
-		s.status = d_status;
-		s.n_pairs = P->n;
+	SerArgs s{};
+	s.ver = d_ver;
+	s.pairs = P->d_pairs.as<PairDev>();
+	s.pplan = P->d_pplan.as<PairPlanDev>();
+	s.rec = P->d_rec.as<uint32_t>();
+	s.n_rec = P->d_nrec.as<uint32_t>();
+	s.crc = P->d_crc.as<uint64_t>();
+	s.offsets = d_offsets;
+	s.out = d_out;
+	s.out_cap = out_cap;
+	s.status = d_status;
+	s.n_pairs = P->n;
+	if (P->ser_block) {
+		// A/B (DG_SER_BLOCK=1): block-per-pair serialiser, CRCs written in place
+		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
 		HIPCHK(ctx, launch_serialize(s, st));
+		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
+		return DG_OK;
 	}
+	// 4. serialise everything but the header CRCs (the CRC stream may still
+	//    be running), then join and patch them in
+	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
+	HIPCHK(ctx, launch_serialize_wave(s, st));
+	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+	HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
 	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
 	return DG_OK;
 }

@@ -206,7 +206,7 @@ struct GlobalSrc {
 	}
 };
 
-constexpr uint32_t kWin = 4096;             // bytes per stream window
+constexpr uint32_t kWin = 3072;             // bytes per stream window (3 KiB: 7.2 KiB LDS per wave, 5 waves/SIMD)
 constexpr uint32_t kLook = 32;              // diagonal batch: lookahead bytes per lane
 constexpr uint32_t kShortT = 12;            // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4

@@ -71,43 +71,64 @@ __device__ __forceinline__ void be32_store(P o, uint32_t x) {
 	o[3] = (uint8_t)x;
 }
 
-// one command per lane (ADD header + short payload + COPY) at base + my;
-// long payloads are copied by the whole wave
-template <typename P>
-__device__ __forceinline__ void put_tile(P base, bool valid, uint32_t my, uint32_t gap, uint32_t prev,
-                                         uint32_t cr, uint32_t cv, uint32_t cl, const uint8_t* V) {
+// kCmd consecutive commands per lane: command i of lane L is record
+// t0 + kCmd*L + i.  `prev0` = end of the command before the lane's first.
+// Writes the lane's commands back to back from base + my; long payloads
+// (> 32 bytes) are copied by the whole wave afterwards.
+template <int kCmd, typename P>
+__device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint32_t my, uint32_t prev0,
+                                         const uint32_t (&cv)[kCmd], const uint32_t (&cr)[kCmd],
+                                         const uint32_t (&cl)[kCmd], const uint8_t* V) {
 	const uint32_t lane = lane_id();
-	bool big = false;
-	if (valid) {
-		P o = base + my;
-		if (gap) {
-			o[0] = 2;
-			be32_store(o + 1, prev);
-			be32_store(o + 5, gap);
-			if (gap <= 32) {
-				for (uint32_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
-			} else {
-				big = true;
+	uint32_t prev = prev0, o = my;
+	bool big[kCmd];
+	uint32_t bsrc[kCmd], blen[kCmd], bdst[kCmd];
+#pragma unroll
+	for (int i = 0; i < kCmd; ++i) {
+		big[i] = false;
+		bsrc[i] = blen[i] = bdst[i] = 0;
+		if (valid[i]) {
+			const uint32_t gap = cv[i] - prev;
+			P q = base + o;
+			if (gap) {
+				q[0] = 2;
+				be32_store(q + 1, prev);
+				be32_store(q + 5, gap);
+				if (gap <= 32) {
+					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = V[prev + k];
+				} else {
+					big[i] = true;
+					bsrc[i] = prev;
+					blen[i] = gap;
+					bdst[i] = o + 9;
+				}
+				q += 9 + gap;
+				o += 9 + gap;
 			}
-			o += 9 + gap;
+			q[0] = 1;
+			be32_store(q + 1, cr[i]);
+			be32_store(q + 5, cv[i]);
+			be32_store(q + 9, cl[i]);
+			o += 13;
+			prev = cv[i] + cl[i];
 		}
-		o[0] = 1;
-		be32_store(o + 1, cr);
-		be32_store(o + 5, cv);
-		be32_store(o + 9, cl);
 	}
-	for (uint64_t bm = __ballot(big); bm; bm &= bm - 1) {
-		const uint32_t k = ffs64(bm);
-		const uint32_t src = rdlane(prev, k), len = rdlane(gap, k), dst = rdlane(my, k) + 9;
-		for (uint32_t i = lane; i < len; i += 64) base[dst + i] = V[src + i];
-	}
+#pragma unroll
+	for (int i = 0; i < kCmd; ++i)
+		for (uint64_t bm = __ballot(big[i]); bm; bm &= bm - 1) {
+			const uint32_t k = ffs64(bm);
+			const uint32_t src = rdlane(bsrc[i], k), len = rdlane(blen[i], k), dst = rdlane(bdst[i], k);
+			for (uint32_t x = lane; x < len; x += 64) base[dst + x] = V[src + x];
+		}
 }
 
 // Wave-wide serialisation of one pair.  `out` = the pair's first output
 // byte, `size` = its delta size (as accumulated by the differencing), `rec`
 // its COPY records (v, r, len) in V order, `stage` >= kStageBytes of LDS.
-// Returns 0, or 5 when the bytes written disagree with `size`.
-template <uint32_t kStageBytes>
+// kCmd records per lane per tile (64 * kCmd commands per tile: fewer
+// dependent load rounds per pair).  Returns 0, or 5 when the bytes written
+// disagree with `size`.
+template <uint32_t kStageBytes, int kCmd = 1>
 __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint8_t* V, uint32_t vl,
                                          const uint32_t* rec, uint32_t n, sw_lds8* stage) {
 	const uint32_t lane = lane_id();
@@ -118,19 +139,37 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 	}
 	uint64_t pos = 25;
 	uint32_t prev_end = 0;   // end of the previous tile's last COPY
-	for (uint32_t t0 = 0; t0 < n; t0 += 64) {
-		const uint32_t j = t0 + lane;
-		const bool valid = j < n;
-		uint32_t cv = 0, cr = 0, cl = 0;
-		if (valid) {
-			cv = rec[3u * j];
-			cr = rec[3u * j + 1];
-			cl = rec[3u * j + 2];
+	for (uint32_t t0 = 0; t0 < n; t0 += 64 * kCmd) {
+		bool valid[kCmd];
+		uint32_t cv[kCmd], cr[kCmd], cl[kCmd];
+#pragma unroll
+		for (int i = 0; i < kCmd; ++i) {
+			const uint32_t j = t0 + kCmd * lane + i;
+			valid[i] = j < n;
+			cv[i] = cr[i] = cl[i] = 0;
+			if (valid[i]) {
+				cv[i] = rec[3u * j];
+				cr[i] = rec[3u * j + 1];
+				cl[i] = rec[3u * j + 2];
+			}
 		}
-		uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)prev_end, (int)(cv + cl), 0x138, 0xF, 0xF, false);
+		// the lane's last valid command end, and the lane's byte count
+		uint32_t last = 0, sz = 0;
+#pragma unroll
+		for (int i = 0; i < kCmd; ++i)
+			if (valid[i]) last = cv[i] + cl[i];
+		uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)prev_end, (int)last, 0x138, 0xF, 0xF, false);
 		if (lane == 0) prev = prev_end;
-		const uint32_t gap = valid ? cv - prev : 0u;
-		const uint32_t sz = valid ? 13u + (gap ? 9u + gap : 0u) : 0u;
+		{
+			uint32_t pv = prev;
+#pragma unroll
+			for (int i = 0; i < kCmd; ++i)
+				if (valid[i]) {
+					const uint32_t gap = cv[i] - pv;
+					sz += 13u + (gap ? 9u + gap : 0u);
+					pv = cv[i] + cl[i];
+				}
+		}
 		// inclusive prefix of the sizes (DPP network; tile bytes < 4 GiB)
 		uint32_t incl = sz;
 		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, false);
@@ -142,7 +181,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 		const uint32_t my = incl - sz;
 		const uint32_t S = rdlane(incl, 63);
 		if (S <= kStageBytes) {
-			put_tile(stage, valid, my, gap, prev, cr, cv, cl, V);
+			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, V);
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // staged bytes are in LDS
 			__builtin_amdgcn_wave_barrier();
 			// flush: head bytes to a dword boundary, dwords, tail bytes
@@ -164,10 +203,14 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // LDS reads done before the next tile
 			__builtin_amdgcn_wave_barrier();
 		} else {
-			put_tile(out + pos, valid, my, gap, prev, cr, cv, cl, V);
+			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, V);
 		}
 		pos += S;
-		prev_end = rdlane(cv + cl, n - 1 - t0 < 63u ? n - 1 - t0 : 63u);
+		prev_end = rdlane(last, 63);
+		{   // lanes past the end hold last = 0: take the highest lane with a command
+			const uint64_t has = __ballot(valid[0]);
+			if (has) prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
+		}
 	}
 	if (prev_end < vl) {   // trailing ADD (src/c/onepass.c:268-275)
 		const uint32_t len = vl - prev_end;

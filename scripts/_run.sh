@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+bash scripts/ab.sh ab14 "DG_SERIAL_CRC=1 -- --config c2" "-- --config c2" "DG_SERIAL_CRC=1 -- --config c3 --steps 5 --warmup 1" "-- --config c3 --steps 5 --warmup 1" "-- --config c5"
