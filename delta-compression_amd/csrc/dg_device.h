@@ -18,7 +18,10 @@ constexpr uint32_t kCrcWavesPerBlock = 4;
 
 // Onepass register history: chunks of 64 steps kept in VGPRs before the
 // epoch spills into a global (slot, tag) table.
-constexpr int kHistChunks = 4;   // 94 VGPRs: 5 waves/SIMD (8 chunks: 113 VGPRs, 4 waves)
+#ifndef DG_HIST_CHUNKS   // tuning knob (make variant): 4 -> 94 VGPRs, 5 waves/SIMD; 8 -> 113, 4 waves
+#define DG_HIST_CHUNKS 4
+#endif
+constexpr int kHistChunks = DG_HIST_CHUNKS;
 
 struct PairDev {          // == dg_pair_t
 	uint64_t r_off, r_len, v_off, v_len;

@@ -594,7 +594,44 @@ __device__ __forceinline__ bool overlap(uint64_t a, uint64_t al, uint64_t b, uin
 	return al && bl && a < b + bl && b < a + al;
 }
 
-constexpr uint32_t kDecWin = 2048;   // LDS window of the command stream
+// Command stream parsing (encoding.c:111-178) is a chain x -> x + |cmd(x)|
+// through the stream.  Per 4 KiB window of the stream (staged in LDS):
+//   1. every lane computes, for each window offset x it owns, the offset of the
+//      next command IF a command started at x (N1), or a code: END, malformed,
+//      header cut by the window, next command past the window;
+//   2. N2 = N1.N1, N4, N8 by pointer doubling (codes propagate);
+//   3. one uniform walk takes 8 commands per step through N8 (single steps
+//      only near the window end), then the nodes in between are expanded in
+//      parallel.
+// So a window of ~300 commands costs ~40 dependent LDS reads instead of ~300
+// serial header decodes.  The commands are then applied 64 at a time.
+#ifdef DG_ONEPASS_PROF   // profiling build only (make prof): per-phase decode cycles
+enum { DP_FILL, DP_LOAD, DP_N1, DP_DBL, DP_WALK, DP_EXP, DP_HDR, DP_COPY, DP_WAIT, DP_WINDOWS, DP_BATCHES, DP_TOTAL, kDecProfN };
+__device__ unsigned long long g_decode_prof[kDecProfN];
+#define DPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define DPROF_ADD(i, t0) (dprof[(i)] += __builtin_amdgcn_s_memtime() - (t0))
+#define DPROF_INC(i) (dprof[(i)] += 1)
+extern "C" int dg_decode_prof_read(unsigned long long* out, int n) {
+	if (n > kDecProfN) n = kDecProfN;
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_decode_prof), 8 * n) == hipSuccess ? n : -1;
+}
+extern "C" int dg_decode_prof_reset(void) {
+	unsigned long long z[kDecProfN] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_decode_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#else
+#define DPROF_T(v) ((void)0)
+#define DPROF_ADD(i, t0) ((void)0)
+#define DPROF_INC(i) ((void)0)
+#endif
+
+constexpr uint32_t kDecWin = 4096;       // bytes of the command stream per window
+constexpr uint32_t kDecMaxCmds = 512;    // >= kDecWin / 9 (the shortest command)
+constexpr uint16_t kNxEnd = 0xFFFE;      // END at x
+constexpr uint16_t kNxBad = 0xFFFD;      // malformed at x
+constexpr uint16_t kNxCut = 0xFFFF;      // header not complete in the window: restart at x
+constexpr uint16_t kNxFar = 0xFFFC;      // complete command at x, next one at/after the window end
+constexpr uint16_t kNxSpecial = 0xFFFC;  // codes are >= this
 
 // inclusive prefix sum over the wave (DPP row shifts + row broadcasts)
 __device__ __forceinline__ uint32_t dec_incl_scan(uint32_t x) {
@@ -607,17 +644,32 @@ __device__ __forceinline__ uint32_t dec_incl_scan(uint32_t x) {
 	return x;
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+	for (int d = 32; d >= 1; d >>= 1) {
+		const uint32_t y = (uint32_t)__shfl_xor((int)x, d, 64);
+		x = x > y ? x : y;
+	}
+	return x;
+}
+
 __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	const uint32_t i = blockIdx.x;
 	if (i >= a.n) return;
 	const uint32_t lane = lane_id();
-	__shared__ uint8_t win[kDecWin + 16];
-	__shared__ uint32_t c_kind[64];
-	__shared__ uint64_t c_src[64], c_dst[64], c_len[64];
-	__shared__ uint32_t c_cum[65];               // flat copy: exclusive byte prefix per command
-	__shared__ const uint8_t* c_sp[64];
-	__shared__ uint8_t* c_dp[64];
+	__shared__ __attribute__((aligned(16))) uint8_t win[kDecWin + 32];
+	__shared__ uint16_t N1[kDecWin], N2[kDecWin], N4[kDecWin], N8[kDecWin];
+	__shared__ uint16_t cmds[kDecMaxCmds];
+	__shared__ uint16_t jumps[kDecMaxCmds / 8 + 1];
+	__shared__ uint32_t c_cum[64];               // flat copy, per non-empty command: byte prefix,
+	__shared__ uint32_t c_row[128];              // row start masks (lo dwords, then hi dwords)
+	__shared__ const uint8_t* c_sp[64];          // source and
+	__shared__ uint8_t* c_dp[64];                // destination
 
+#ifdef DG_ONEPASS_PROF
+	uint64_t dprof[kDecProfN] = {};
+	const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
 	const dg_decode_desc_dev dd = a.descs[i];
 	const uint8_t* D = a.delta + dd.delta_off;
 	const uint64_t dl = dd.delta_len;
@@ -645,6 +697,7 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	}
 	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
 	const uint64_t init = inplace ? (rl < bsz ? rl : bsz) : 0;
+	DPROF_T(tf0);
 	{
 		uint64_t k0 = 0;
 		if ((((uintptr_t)O | (uintptr_t)R) & 15) == 0) {   // 16 B per lane, 4 in flight
@@ -671,142 +724,294 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	}
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	__builtin_amdgcn_wave_barrier();
+	DPROF_ADD(DP_FILL, tf0);
 
-	uint64_t pos = 25;          // next unparsed byte of the stream
-	uint64_t wbase = ~0ull;     // stream offset of win[0]
+	uint64_t pos = 25;   // stream offset of the current window: a command boundary
 	bool done = false;
+	uint32_t hwm = 0;    // end of the highest destination written while every batch stayed ordered
 	while (!done && !st) {
-		// ── lane 0 parses up to 64 commands (LDS window refilled as needed) ──
-		uint32_t cnt = 0;
-		while (cnt < 64 && !done && !st) {
-			if (pos >= dl) { done = true; break; }   // missing END: end of input
-			if (wbase == ~0ull || pos < wbase || pos + 13 > wbase + kDecWin) {
-				wbase = pos;
-				__builtin_amdgcn_wave_barrier();
-				for (uint32_t k = lane; k < kDecWin; k += 64) win[k] = wbase + k < dl ? D[wbase + k] : 0;
-				__syncthreads();
-			}
-			const uint8_t* w = win + (pos - wbase);
-			const uint32_t t = w[0];
-			if (t == 0) { done = true; break; }
-			if (t == 1) {
-				if (pos + 13 > dl) { st = 8; break; }
-				if (lane == 0) {
-					c_kind[cnt] = 1;
-					c_src[cnt] = be32(w + 1);
-					c_dst[cnt] = be32(w + 5);
-					c_len[cnt] = be32(w + 9);
-				}
-				pos += 13;
-			} else if (t == 2) {
-				if (pos + 9 > dl) { st = 8; break; }
-				const uint64_t len = be32(w + 5);
-				if (pos + 9 + len > dl) { st = 8; break; }
-				if (lane == 0) {
-					c_kind[cnt] = 2;
-					c_src[cnt] = pos + 9;   // payload offset in the stream
-					c_dst[cnt] = be32(w + 1);
-					c_len[cnt] = len;
-				}
-				pos += 9 + len;
-			} else {
-				st = 8;
-				break;
-			}
-			++cnt;
+		if (pos >= dl) break;   // missing END: end of input (as the reference's loop)
+		const uint32_t avail = (uint32_t)min((uint64_t)kDecWin, dl - pos);
+		// ── 1. window -> LDS: aligned 16-byte blocks that hold stream bytes
+		//    (a block never crosses a page), win[sh + x] = D[pos + x]
+		const uintptr_t wa = (uintptr_t)(D + pos) & ~(uintptr_t)15;
+		const uint32_t sh = (uint32_t)((uintptr_t)(D + pos) - wa);
+		const uintptr_t dend = (uintptr_t)(D + dl);
+		DPROF_INC(DP_WINDOWS);
+		DPROF_T(tl0);
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		for (uint32_t q = lane; q < (kDecWin + 32) / 16; q += 64) {
+			const uintptr_t ad = wa + 16 * q;
+			uint4 x = make_uint4(0, 0, 0, 0);
+			if (ad < dend) x = *reinterpret_cast<const uint4*>(ad);
+			reinterpret_cast<uint4*>(win)[q] = x;
 		}
-		__syncthreads();
-		if (st || cnt == 0) break;
-
-		// ── apply the batch ──
-		const bool mine = lane < cnt;
-		const uint32_t kind = mine ? c_kind[lane] : 0;
-		const uint64_t src = mine ? c_src[lane] : 0, dst = mine ? c_dst[lane] : 0, len = mine ? c_len[lane] : 0;
-		bool bad = false;
-		if (mine) {
-			if (dst + len > bsz) bad = true;
-			if (kind == 1 && src + len > (inplace ? bsz : rl)) bad = true;
-		}
-		if (__ballot(bad)) { st = 8; break; }
-		// conflicts with earlier commands of the batch (writes vs writes; and
-		// in-place: writes vs reads both ways)
-		bool conflict = false;
-		const bool reads_buf = inplace && kind == 1;
-		for (uint32_t k = 0; k + 1 < cnt; ++k) {
-			const uint64_t ks = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)src, k)) |
-			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(src >> 32), k) << 32);
-			const uint64_t kd = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)dst, k)) |
-			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(dst >> 32), k) << 32);
-			const uint64_t kl = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)len, k)) |
-			                    ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(len >> 32), k) << 32);
-			const bool kreads = inplace && rdlane(kind, k) == 1;
-			if (mine && lane > k) {
-				if (overlap(kd, kl, dst, len)) conflict = true;
-				if (reads_buf && overlap(kd, kl, src, len)) conflict = true;
-				if (kreads && overlap(ks, kl, dst, len)) conflict = true;
-			}
-		}
-		if (__ballot(conflict) == 0) {
-			// Independent commands.  An in-place COPY whose source and
-			// destination overlap keeps its memmove (src == dst is a no-op).
-			// Every other byte of the batch is copied in one flat pass: byte j
-			// of the batch's concatenation goes to lane j % 64, with 16 loads
-			// per lane in flight before their stores and no wait between
-			// commands (the previous form waited twice per command > 64 B).
-			const uint8_t* sp = kind == 1 ? (inplace ? O + src : R + src) : D + src;
-			const bool selfov = mine && kind == 1 && inplace && src != dst && overlap(src, len, dst, len);
-			const bool noop = mine && kind == 1 && inplace && src == dst;
-			const uint32_t flen = (mine && !selfov && !noop) ? (uint32_t)len : 0u;
-			const uint32_t incl = dec_incl_scan(flen);
-			c_cum[lane] = incl - flen;
-			if (lane == 63) c_cum[64] = incl;
-			c_sp[lane] = sp;
-			c_dp[lane] = O + dst;
-			__builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-			__builtin_amdgcn_wave_barrier();
-			const uint32_t total = rdlane(incl, 63);
-			uint32_t k = 0;
-			constexpr int kU = 16;
-			for (uint32_t b0 = 0; b0 < total; b0 += 64 * kU) {
-				uint8_t v[kU];
-				uint8_t* d[kU];
-#pragma unroll
-				for (int u = 0; u < kU; ++u) {
-					const uint32_t j = b0 + 64 * u + lane;
-					d[u] = nullptr;
-					if (j < total) {
-						while (c_cum[k + 1] <= j) ++k;
-						const uint32_t off = j - c_cum[k];
-						v[u] = c_sp[k][off];
-						d[u] = c_dp[k] + off;
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		const uint8_t* w = win + sh;
+		DPROF_ADD(DP_LOAD, tl0);
+		DPROF_T(tn0);
+		// ── 2. N1: next command offset for a command starting at x ──
+		for (uint32_t x = lane; x < kDecWin; x += 64) {
+			uint16_t nx = kNxBad;
+			if (x < avail) {
+				const uint32_t t = w[x];
+				if (t == 0) {
+					nx = kNxEnd;
+				} else if (t == 1 || t == 2) {
+					const uint32_t hdr = t == 1 ? 13u : 9u;
+					if (x + hdr > avail) {
+						nx = pos + x + hdr > dl ? kNxBad : kNxCut;
+					} else {
+						const uint64_t len = t == 1 ? 0 : be32(w + x + 5);
+						const uint64_t end = (uint64_t)x + hdr + len;
+						if (pos + end > dl) nx = kNxBad;
+						else nx = end >= avail ? kNxFar : (uint16_t)end;
 					}
 				}
+			}
+			N1[x] = nx;
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		DPROF_ADD(DP_N1, tn0);
+		DPROF_T(td0);
+		// ── 3. pointer doubling ──
+		for (uint32_t x = lane; x < kDecWin; x += 64) {
+			const uint16_t y = N1[x];
+			N2[x] = y >= kNxSpecial ? y : N1[y];
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		for (uint32_t x = lane; x < kDecWin; x += 64) {
+			const uint16_t y = N2[x];
+			N4[x] = y >= kNxSpecial ? y : N2[y];
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		for (uint32_t x = lane; x < kDecWin; x += 64) {
+			const uint16_t y = N4[x];
+			N8[x] = y >= kNxSpecial ? y : N4[y];
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		DPROF_ADD(DP_DBL, td0);
+		DPROF_T(tw0);
+		// ── 4. the walk (uniform): 8 commands per N8 step, then single steps ──
+		uint32_t x = 0, nj = 0;
+		uint16_t term = 0;   // the code that ended the walk
+		while (true) {
+			const uint32_t y = uni(N8[x]);
+			if (y >= kNxSpecial || 8 * (nj + 1) > kDecMaxCmds) break;
+			if (lane == 0) jumps[nj] = (uint16_t)x;
+			++nj;
+			x = y;
+		}
+		uint32_t cnt = 8 * nj;
+		while (true) {   // single steps from x (at most 7 commands + the terminal)
+			const uint32_t y = uni(N1[x]);
+			if (y == kNxEnd || y == kNxBad || y == kNxCut) { term = (uint16_t)y; break; }
+			if (cnt >= kDecMaxCmds) { term = kNxCut; break; }   // restart the window at x
+			if (lane == 0) cmds[cnt] = (uint16_t)x;
+			++cnt;
+			if (y == kNxFar) { term = kNxFar; break; }
+			x = y;
+		}
+		DPROF_ADD(DP_WALK, tw0);
+		DPROF_T(te0);
+		// expand the jumps: the 8 nodes from jumps[j]
+		for (uint32_t j = lane; j < nj; j += 64) {
+			const uint32_t e0 = jumps[j];
+			const uint32_t e2 = N2[e0], e4 = N4[e0];
+			const uint32_t e6 = N2[e4];
+			uint16_t* c = cmds + 8 * j;
+			c[0] = (uint16_t)e0;
+			c[1] = N1[e0];
+			c[2] = (uint16_t)e2;
+			c[3] = N1[e2];
+			c[4] = (uint16_t)e4;
+			c[5] = N1[e4];
+			c[6] = (uint16_t)e6;
+			c[7] = N1[e6];
+		}
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		DPROF_ADD(DP_EXP, te0);
+		// the walk's terminal: x is where it stopped
+		uint64_t next_pos = pos + x;   // kNxCut: restart at x
+		if (term == kNxEnd) done = true;
+		else if (term == kNxBad) st = 8;
+		else if (term == kNxFar) {
+			const uint32_t t = w[x];
+			next_pos = pos + x + (t == 1 ? 13u : 9u + be32(w + x + 5));
+		}
+		if (term == kNxCut && cnt == 0 && x == 0) st = 8;   // cannot happen: a header fits 4 KiB
+
+		// ── 5. apply the window's commands, 64 at a time ──
+		for (uint32_t b = 0; b < cnt && !st; b += 64) {
+			DPROF_INC(DP_BATCHES);
+			DPROF_T(th0);
+			const bool mine = b + lane < cnt;
+			uint32_t kind = 0;
+			uint64_t src = 0, dst = 0, len = 0;
+			if (mine) {
+				const uint32_t cx = cmds[b + lane];
+				kind = w[cx];
+				if (kind == 1) {
+					src = be32(w + cx + 1);
+					dst = be32(w + cx + 5);
+					len = be32(w + cx + 9);
+				} else {
+					src = pos + cx + 9;   // payload offset in the stream
+					dst = be32(w + cx + 1);
+					len = be32(w + cx + 5);
+				}
+			}
+			bool bad = false;
+			if (mine) {
+				if (dst + len > bsz) bad = true;
+				if (kind == 1 && src + len > (inplace ? bsz : rl)) bad = true;
+			}
+			if (__ballot(bad)) { st = 8; break; }
+			// conflicts among the batch's commands (writes vs writes; and
+			// in-place: writes vs reads both ways).  Fast proof: destinations
+			// in increasing, disjoint order and no in-place COPY that moves.
+			const uint32_t end32 = (uint32_t)(dst + len), dst32 = (uint32_t)dst;   // < 2^32 (bsz checked)
+			uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end32, 0x138, 0xF, 0xF, false);
+			const bool unordered = mine && ((lane > 0 && dst32 < prev_end) || (lane == 0 && dst32 < hwm));
+			const bool moves = mine && inplace && kind == 1 && src != dst;
+			// ordered after everything applied so far: no wait needed before
+			// the next batch (no byte written twice, no buffer byte read)
+			const bool after_all = __ballot(unordered || moves) == 0;
+			bool conflict = false;
+			if (!after_all) {
+				// earlier batches may still have stores in flight that this one
+				// reads or overwrites
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				__builtin_amdgcn_wave_barrier();
+				const bool reads_buf = inplace && kind == 1;
+				const uint32_t n = cnt - b < 64 ? cnt - b : 64;
+				for (uint32_t k = 0; k + 1 < n; ++k) {
+					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), k) << 32) | rdlane((uint32_t)src, k);
+					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), k) << 32) | rdlane((uint32_t)dst, k);
+					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), k) << 32) | rdlane((uint32_t)len, k);
+					const bool kreads = inplace && rdlane(kind, k) == 1;
+					if (mine && lane > k) {
+						if (overlap(kd, kl, dst, len)) conflict = true;
+						if (reads_buf && overlap(kd, kl, src, len)) conflict = true;
+						if (kreads && overlap(ks, kl, dst, len)) conflict = true;
+					}
+				}
+			}
+			DPROF_ADD(DP_HDR, th0);
+			DPROF_T(tc0);
+			if (__ballot(conflict) == 0) {
+				// Independent commands.  An in-place COPY whose source and
+				// destination overlap keeps its memmove (src == dst is a no-op).
+				// Every other byte of the batch is copied in one flat pass: byte
+				// j of the batch's concatenation goes to lane j % 64, with 16
+				// loads per lane in flight before their stores.
+				const uint8_t* sp = kind == 1 ? (inplace ? O + src : R + src) : D + src;
+				const bool selfov = mine && kind == 1 && inplace && src != dst && overlap(src, len, dst, len);
+				const bool noop = mine && kind == 1 && inplace && src == dst;
+				const uint32_t flen = (mine && !selfov && !noop) ? (uint32_t)len : 0u;
+				// Element j of the batch's byte concatenation is done by lane
+				// j % 64 in row j / 64.  The command owning j is found without a
+				// walk: rows carry a 64-bit mask of where non-empty commands
+				// start, so owner = (starts before the row) + popcount(mask
+				// bits <= lane) - 1, an ordinal into the non-empty commands.
+				const uint32_t incl = dec_incl_scan(flen);
+				const uint32_t cum = incl - flen;
+				const uint32_t total = rdlane(incl, 63);
+				const bool nz = flen != 0;
+				const uint32_t ord = dec_incl_scan(nz ? 1u : 0u) - 1u;
+				if (nz) {
+					c_cum[ord] = cum;
+					c_sp[ord] = sp;
+					c_dp[ord] = O + dst;
+				}
+				typedef __attribute__((address_space(1))) const uint8_t gcu8;
+				typedef __attribute__((address_space(1))) uint8_t gu8;
+				for (uint32_t r0 = 0; 64 * r0 < total; r0 += 64) {   // 64 rows = 4 KiB per round
+					// start masks of rows r0 .. r0+63 (LDS, as two dwords per row)
+					c_row[lane] = 0;
+					c_row[64 + lane] = 0;
+					__builtin_amdgcn_s_waitcnt(0xc07f);
+					__builtin_amdgcn_wave_barrier();
+					if (nz && cum >= 64 * r0 && cum < 64 * (r0 + 64)) {
+						const uint32_t row = cum / 64 - r0, bit = cum % 64;
+						atomicOr(&c_row[(bit >> 5) * 64 + row], 1u << (bit & 31));
+					}
+					const uint32_t carry = (uint32_t)__builtin_popcountll(__ballot(nz && cum < 64 * r0));
+					__builtin_amdgcn_s_waitcnt(0xc07f);
+					__builtin_amdgcn_wave_barrier();
+					const uint64_t mrow = ((uint64_t)c_row[64 + lane] << 32) | c_row[lane];   // row r0 + lane
+					const uint32_t pc = (uint32_t)__builtin_popcountll(mrow);
+					const uint32_t rbase = carry + dec_incl_scan(pc) - pc;   // starts before row r0 + lane
+					const uint32_t nrows = min(64u, (total + 63) / 64 - r0);
+					uint32_t o[64];
+					uint8_t v[64];
 #pragma unroll
-				for (int u = 0; u < kU; ++u)
-					if (d[u]) *d[u] = v[u];
+					for (int u = 0; u < 64; ++u) {
+						const uint32_t j = 64 * (r0 + u) + lane;
+						o[u] = 0xFFFFFFFFu;
+						if ((uint32_t)u < nrows && j < total) {
+							const uint64_t m = ((uint64_t)rdlane((uint32_t)(mrow >> 32), u) << 32) | rdlane((uint32_t)mrow, u);
+							o[u] = rdlane(rbase, u) + (uint32_t)__builtin_popcountll(m & mask_le(lane)) - 1u;
+							v[u] = *(gcu8*)(c_sp[o[u]] + (j - c_cum[o[u]]));
+						}
+					}
+#pragma unroll
+					for (int u = 0; u < 64; ++u) {
+						const uint32_t j = 64 * (r0 + u) + lane;
+						if (o[u] != 0xFFFFFFFFu) *(gu8*)(c_dp[o[u]] + (j - c_cum[o[u]])) = v[u];
+					}
+				}
+				for (uint64_t m = __ballot(selfov); m; m &= m - 1) {
+					const uint32_t kk = ffs64(m);
+					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), kk) << 32) | rdlane((uint32_t)src, kk);
+					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), kk) << 32) | rdlane((uint32_t)dst, kk);
+					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), kk) << 32) | rdlane((uint32_t)len, kk);
+					wave_memmove(O + kd, O + ks, kl);
+				}
+			} else {
+				// strict stream order (apply.c:257-266)
+				const uint32_t n = cnt - b < 64 ? cnt - b : 64;
+				for (uint32_t k = 0; k < n; ++k) {
+					const uint32_t kk = rdlane(kind, k);
+					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), k) << 32) | rdlane((uint32_t)src, k);
+					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), k) << 32) | rdlane((uint32_t)dst, k);
+					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), k) << 32) | rdlane((uint32_t)len, k);
+					wave_memmove(O + kd, kk == 1 ? (inplace ? O + ks : R + ks) : D + ks, kl);
+				}
 			}
-			for (uint64_t m = __ballot(selfov); m; m &= m - 1) {
-				const uint32_t kk = ffs64(m);
-				const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), kk) << 32) | rdlane((uint32_t)src, kk);
-				const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), kk) << 32) | rdlane((uint32_t)dst, kk);
-				const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), kk) << 32) | rdlane((uint32_t)len, kk);
-				wave_memmove(O + kd, O + ks, kl);
-			}
-		} else {
-			// strict stream order (apply.c:257-266)
-			for (uint32_t k = 0; k < cnt; ++k) {
-				const uint32_t kk = c_kind[k];
-				wave_memmove(O + c_dst[k], kk == 1 ? (inplace ? O + c_src[k] : R + c_src[k]) : D + c_src[k], c_len[k]);
+			DPROF_ADD(DP_COPY, tc0);
+			if (after_all) {
+				hwm = uni(wave_max_u32(mine ? end32 : 0u)) > hwm ? uni(wave_max_u32(mine ? end32 : 0u)) : hwm;
+			} else {
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				__builtin_amdgcn_wave_barrier();
+				hwm = 0xFFFFFFFFu;   // order unknown from here: every later batch waits
 			}
 		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
+		pos = next_pos;
 	}
 	if (lane == 0) {
 		a.status[i] = st;
 		a.out_len[i] = st ? 0 : vsize;
 		if (a.out_spans) a.out_spans[i].len = st ? 0 : vsize;
 	}
+#ifdef DG_ONEPASS_PROF
+	{
+		DPROF_T(tw9);
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		DPROF_ADD(DP_WAIT, tw9);
+		dprof[DP_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
+		if (lane == 0)
+			for (int k = 0; k < kDecProfN; ++k) atomicAdd(&g_decode_prof[k], (unsigned long long)dprof[k]);
+	}
+#endif
 }
 
 // CRC checks after decoding, in the reference's order of precedence: a

@@ -206,8 +206,17 @@ struct GlobalSrc {
 	}
 };
 
-constexpr uint32_t kWin = 3072;             // bytes per stream window (3 KiB: 7.2 KiB LDS per wave, 5 waves/SIMD)
-constexpr uint32_t kLook = 32;              // diagonal batch: lookahead bytes per lane
+#ifndef DG_WIN_BYTES      // tuning knobs (make variant); window: a multiple of 16, >= 64 * kLook + 48
+#define DG_WIN_BYTES 3072
+#endif
+#ifndef DG_LOOK_BYTES
+#define DG_LOOK_BYTES 32
+#endif
+#ifndef DG_WAVES_PER_EU
+#define DG_WAVES_PER_EU 5
+#endif
+constexpr uint32_t kWin = DG_WIN_BYTES;     // bytes per stream window (3 KiB: 7.2 KiB LDS per wave, 5 waves/SIMD)
+constexpr uint32_t kLook = DG_LOOK_BYTES;   // diagonal batch: lookahead bytes per lane
 constexpr uint32_t kShortT = 12;            // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 
@@ -237,9 +246,9 @@ struct WinSrc {
 		if (fv) {
 			const uint32_t nb = vlo & ~15u;
 #pragma unroll
-			for (uint32_t k = 0; k < kWin / 1024; ++k) {
+			for (uint32_t k = 0; k < (kWin + 1023) / 1024; ++k) {
 				const uint32_t off = nb + 1024 * k + 16 * lane;
-				if (off < len[0])
+				if (off < len[0] && 1024 * k + 16 * lane < kWin)
 					__builtin_amdgcn_global_load_lds((const void*)(S[0] + off),
 					                                 (lds_void_t*)(win + 1024 * k), 16, 0, 0);
 			}
@@ -248,9 +257,9 @@ struct WinSrc {
 		if (fr) {
 			const uint32_t nb = rlo & ~15u;
 #pragma unroll
-			for (uint32_t k = 0; k < kWin / 1024; ++k) {
+			for (uint32_t k = 0; k < (kWin + 1023) / 1024; ++k) {
 				const uint32_t off = nb + 1024 * k + 16 * lane;
-				if (off < len[1])
+				if (off < len[1] && 1024 * k + 16 * lane < kWin)
 					__builtin_amdgcn_global_load_lds((const void*)(S[1] + off),
 					                                 (lds_void_t*)(win + kWinStride + 1024 * k), 16, 0, 0);
 			}
@@ -837,7 +846,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 }
 
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
-__global__ __launch_bounds__(64, 4) void onepass16_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch list, member table, round bitmaps
 	const uint32_t pair = blockIdx.x;
