@@ -21,31 +21,44 @@ namespace dg {
 
 // ───────────────────────────── scan of sizes ──────────────────────────────
 
+// One block: each thread sums a contiguous run of ceil(n / 1024) sizes, the
+// block scans the 1024 run sums (wave shuffles + 16 wave totals in LDS), and
+// each thread writes its run's exclusive offsets.  One barrier pair.
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
+	const uint32_t lane = lane_id();
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d, 64);
+		const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d, 64);
+		if (lane >= (uint32_t)d) x += ((uint64_t)hi << 32) | lo;
+	}
+	return x;
+}
+
 __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __restrict__ sz,
                                                           uint64_t* __restrict__ off,
                                                           uint32_t n) {
-	__shared__ uint64_t buf[1024];
-	__shared__ uint64_t carry;
-	const uint32_t tid = threadIdx.x;
-	if (tid == 0) carry = 0;
+	__shared__ uint64_t wsum[16];
+	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+	const uint32_t per = (n + 1023) / 1024;
+	const uint32_t b = tid * per, e = min(b + per, n);
+	uint64_t s = 0;
+	for (uint32_t k = b; k < e; ++k) s += sz[k];
+	const uint64_t incl = wave_incl_scan64(s);
+	if (lane == 63) wsum[wave] = incl;
 	__syncthreads();
-	for (uint32_t base = 0; base < n; base += 1024) {
-		const uint64_t x = base + tid < n ? sz[base + tid] : 0;
-		buf[tid] = x;
-		__syncthreads();
-		for (uint32_t d = 1; d < 1024; d <<= 1) {
-			const uint64_t y = tid >= d ? buf[tid - d] : 0;
-			__syncthreads();
-			buf[tid] += y;
-			__syncthreads();
-		}
-		const uint64_t c = carry;
-		if (base + tid < n) off[base + tid] = c + buf[tid] - x;
-		__syncthreads();
-		if (tid == 1023) carry = c + buf[1023];
-		__syncthreads();
+	if (wave == 0) {
+		const uint64_t w = lane < 16 ? wsum[lane] : 0;
+		const uint64_t wi = wave_incl_scan64(w);
+		if (lane < 16) wsum[lane] = wi - w;   // exclusive wave offsets
 	}
-	if (tid == 0) off[n] = carry;
+	__syncthreads();
+	uint64_t run = wsum[wave] + incl - s;
+	for (uint32_t k = b; k < e; ++k) {
+		off[k] = run;
+		run += sz[k];
+	}
+	if (tid == 1023) off[n] = wsum[15] + incl;   // the grand total (thread 1023 holds the last run)
 }
 
 // ───────────────────────────── serialisation ──────────────────────────────

@@ -66,12 +66,19 @@ enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATC
 __device__ unsigned long long g_onepass_prof[kProfN];
 #define PROF_DECL uint64_t prof[kProfN];
 #define PROF_INIT(o) for (int _i = 0; _i < kProfN; ++_i) (o).prof[_i] = 0;
+#ifdef DG_ONEPASS_PROF_LITE   // only the refill wait, the epoch counts and the total are timed
+#define PROF_NOW() 0ull
+#define PROF_NOW_R() ((uint64_t)__builtin_amdgcn_s_memtime())
+#else
 #define PROF_NOW() ((uint64_t)clock64())
+#define PROF_NOW_R() ((uint64_t)clock64())
+#endif
 #define PROF_ADD(o, i, v) ((o).prof[(i)] += (uint64_t)(v))
 #else
 #define PROF_DECL
 #define PROF_INIT(o)
 #define PROF_NOW() 0ull
+#define PROF_NOW_R() 0ull
 #define PROF_ADD(o, i, v) ((void)0)
 #endif
 
@@ -236,7 +243,7 @@ struct WinSrc {
 		const bool fv = wantV && (vlo < base[0] || vlo + need > base[0] + kWin);
 		const bool fr = wantR && (rlo < base[1] || rlo + need > base[1] + kWin);
 		if (!fv && !fr) return;
-		[[maybe_unused]] const uint64_t t0 = PROF_NOW();
+		[[maybe_unused]] const uint64_t t0 = PROF_NOW_R();
 		const uint32_t lane = lane_id();
 		__syncthreads();   // the wave's reads of the old window are complete
 		// lane l's 16 bytes land at lds + 16*l (lane-linear).  Blocks past the
@@ -268,7 +275,7 @@ struct WinSrc {
 		vm_drain();        // the DMA landed (ordered by vmcnt) ...
 		__syncthreads();   // ... and is visible to every lane
 		PROF_ADD(*this, P_REFILLS, 1);
-		PROF_ADD(*this, P_T_REFILL, PROF_NOW() - t0);
+		PROF_ADD(*this, P_T_REFILL, PROF_NOW_R() - t0);
 	}
 
 	// 4 bytes of stream s at offset x (little-endian), x inside the window
@@ -865,7 +872,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	src.win = (lds_u8*)win;
 	src.powc = a.powc;
 	PROF_INIT(src)
-	[[maybe_unused]] const uint64_t t_start = PROF_NOW();
+	[[maybe_unused]] const uint64_t t_start = PROF_NOW_R();
 	uint64_t cA[4];
 	const uint32_t part = lane_id() & 3u;
 #pragma unroll
@@ -891,7 +898,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 		if (lane == 0 && st != res.st) a.status[pair] = st;
 	}
 #ifdef DG_ONEPASS_PROF
-	if (lane_id() == 0) atomicAdd(&g_onepass_prof[P_T_TOTAL], (unsigned long long)(PROF_NOW() - t_start));
+	if (lane_id() == 0) atomicAdd(&g_onepass_prof[P_T_TOTAL], (unsigned long long)(PROF_NOW_R() - t_start));
 #endif
 }
 

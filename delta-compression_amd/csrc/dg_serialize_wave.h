@@ -139,6 +139,19 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 	}
 	uint64_t pos = 25;
 	uint32_t prev_end = 0;   // end of the previous tile's last COPY
+	// the next tile's records are loaded while this tile is assembled: their
+	// latency hides under this tile's payload loads
+	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd];
+#pragma unroll
+	for (int i = 0; i < kCmd; ++i) {
+		const uint32_t j = kCmd * lane + i;
+		ncv[i] = ncr[i] = ncl[i] = 0;
+		if (j < n) {
+			ncv[i] = rec[3u * j];
+			ncr[i] = rec[3u * j + 1];
+			ncl[i] = rec[3u * j + 2];
+		}
+	}
 	for (uint32_t t0 = 0; t0 < n; t0 += 64 * kCmd) {
 		bool valid[kCmd];
 		uint32_t cv[kCmd], cr[kCmd], cl[kCmd];
@@ -146,11 +159,15 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 		for (int i = 0; i < kCmd; ++i) {
 			const uint32_t j = t0 + kCmd * lane + i;
 			valid[i] = j < n;
-			cv[i] = cr[i] = cl[i] = 0;
-			if (valid[i]) {
-				cv[i] = rec[3u * j];
-				cr[i] = rec[3u * j + 1];
-				cl[i] = rec[3u * j + 2];
+			cv[i] = ncv[i];
+			cr[i] = ncr[i];
+			cl[i] = ncl[i];
+			const uint32_t jn = j + 64 * kCmd;
+			ncv[i] = ncr[i] = ncl[i] = 0;
+			if (jn < n) {
+				ncv[i] = rec[3u * jn];
+				ncr[i] = rec[3u * jn + 1];
+				ncl[i] = rec[3u * jn + 2];
 			}
 		}
 		// the lane's last valid command end, and the lane's byte count
