@@ -230,7 +230,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 	const uint32_t bc = uni(a.buf_cap ? a.buf_cap : 1u);
 	const uint32_t rcap = bc + 1;
 	const uint32_t rec_cap = uni(pp.rec_cap);
-	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
+	uint32_t* __restrict__ rec = a.rec + (uint64_t)kRecWordsCorrecting * pp.rec_base;
 
 	uint32_t nrec = 0, head = 0, n = 0;
 	uint64_t dsz = 26;   // header + END

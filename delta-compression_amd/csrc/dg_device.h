@@ -90,11 +90,18 @@ struct EncodeArgs {
 	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
 };
 
+// COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the
+// first 4 bytes of V from the gap start (the end of the previous COPY), so a
+// gap of <= 4 bytes serialises without reading V (at C2 nearly every ADD).
+constexpr uint32_t kRecWordsOnepass = 4;
+constexpr uint32_t kRecWordsCorrecting = 3;
+
 struct SerArgs {
 	const uint8_t* ver;
 	const PairDev* pairs;
 	const PairPlanDev* pplan;
 	const uint32_t* rec;
+	uint32_t rec_words;        // 3 or 4 (kRecWords*)
 	const uint32_t* n_rec;
 	const uint64_t* crc;       // 2 per pair: R, V
 	const uint64_t* offsets;   // n+1

@@ -445,7 +445,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_pairs.alloc(sizeof(PairDev) * std::max<uint32_t>(n, 1));
 	bad |= P->d_pplan.alloc(sizeof(PairPlanDev) * std::max<uint32_t>(n, 1));
 	bad |= P->d_powc.alloc(8 * p);
-	bad |= P->d_rec.alloc(12 * std::max<uint64_t>(rec, 1));
+	bad |= P->d_rec.alloc(4ull * (algo == DG_ALGO_ONEPASS ? kRecWordsOnepass : kRecWordsCorrecting) *
+	                      std::max<uint64_t>(rec, 1));
 	bad |= P->d_nrec.alloc(4ull * std::max<uint32_t>(n, 1));
 	bad |= P->d_dsize.alloc(8ull * std::max<uint32_t>(n, 1));
 	bad |= P->d_crc_spans_r.alloc(sizeof(CrcSpanDev) * std::max<size_t>(sd.size(), 1));
@@ -675,6 +676,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	s.pairs = P->d_pairs.as<PairDev>();
 	s.pplan = P->d_pplan.as<PairPlanDev>();
 	s.rec = P->d_rec.as<uint32_t>();
+	s.rec_words = P->algo == DG_ALGO_ONEPASS ? kRecWordsOnepass : kRecWordsCorrecting;
 	s.n_rec = P->d_nrec.as<uint32_t>();
 	s.crc = P->d_crc.as<uint64_t>();
 	s.offsets = d_offsets;

@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 	const uint8_t* V = s.ver + pd.v_off;
 	const uint64_t vl = pd.v_len;
 	const uint32_t n = s.n_rec[pair];
-	const uint32_t* rec = s.rec + 3ull * pp.rec_base;
+	const uint32_t W = s.rec_words;
+	const uint32_t* rec = s.rec + (uint64_t)W * pp.rec_base;
 	uint8_t* out = s.out + base;
 
 	if (tid == 0) {
@@ -134,8 +135,8 @@ __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 		uint32_t cv = 0, cr = 0, cl = 0;
 		uint64_t prev = 0;
 		if (valid) {
-			cv = rec[3u * j]; cr = rec[3u * j + 1]; cl = rec[3u * j + 2];
-			if (j > 0) prev = (uint64_t)rec[3u * (j - 1)] + rec[3u * (j - 1) + 2];
+			cv = rec[W * j]; cr = rec[W * j + 1]; cl = rec[W * j + 2];
+			if (j > 0) prev = (uint64_t)rec[W * (j - 1)] + rec[W * (j - 1) + 2];
 		}
 		const uint64_t gap = valid ? cv - prev : 0;
 		const uint64_t sz = valid ? 13 + (gap ? 9 + gap : 0) : 0;
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 	}
 
 	uint64_t pos = pos_sh;
-	const uint64_t last = n ? (uint64_t)rec[3u * (n - 1)] + rec[3u * (n - 1) + 2] : 0;
+	const uint64_t last = n ? (uint64_t)rec[W * (n - 1)] + rec[W * (n - 1) + 2] : 0;
 	if (last < vl) {   // trailing ADD
 		const uint64_t len = vl - last;
 		if (tid == 0) {
@@ -495,8 +496,8 @@ __global__ __launch_bounds__(64) void serialize_wave_kernel(SerArgs s) {
 	const PairDev pd = s.pairs[pair];
 	const PairPlanDev pp = s.pplan[pair];
 	const int32_t st = serialize_wave<kSerWaveStage, kSerWaveCmds>(s.out + base, end - base, s.ver + pd.v_off,
-	                                                 (uint32_t)pd.v_len, s.rec + 3ull * pp.rec_base,
-	                                                 s.n_rec[pair], (sw_lds8*)stage);
+	                                                 (uint32_t)pd.v_len, s.rec + (uint64_t)s.rec_words * pp.rec_base,
+	                                                 s.rec_words, s.n_rec[pair], (sw_lds8*)stage);
 	if (st != 0 && lane_id() == 0) s.status[pair] = st;
 }
 

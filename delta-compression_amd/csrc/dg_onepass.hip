@@ -518,10 +518,11 @@ struct WinSrc {
 			if (lane < fm) {
 				const uint32_t w = mlist[64 + lane];
 				const uint32_t ms = w & 2047u, me = (w >> 11) & 4095u, mt = w >> 23;
-				uint32_t* o = rec + 3u * (nrec + committed + lane);
+				uint32_t* o = rec + kRecWordsOnepass * (nrec + committed + lane);
 				o[0] = v0 + ms + mt;
 				o[1] = r0 + ms + mt;
 				o[2] = me - ms - mt;
+				o[3] = rd4(0, v0 + ms);   // the ADD's first bytes (gap start = member start)
 			}
 			// sum over committed members of (T + 1) is the first lane of member fm
 			dadd += 21u * fm + fbad;
@@ -583,7 +584,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
 	const uint32_t rec_cap = uni(pp.rec_cap);
-	uint32_t* __restrict__ rec = a.rec + 3ull * pp.rec_base;
+	uint32_t* __restrict__ rec = a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base;
 
 	uint32_t nrec = 0;
 	uint64_t dsz = 26;   // header (25) + END
@@ -629,12 +630,14 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 		bool matched = false;
 		uint32_t vm = 0, rm = 0, ml = 0;
+		uint32_t pw = 0;   // 4th record word
 
 		// ── phase A: steps 0..7, four lanes per window ──
 		if constexpr (Src::kPhaseA) {
 			[[maybe_unused]] const uint64_t ta = PROF_NOW();
 			PROF_ADD(src, P_A_ENTRIES, 1);
 			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
+			pw = uni(src.rd4(0, v0));   // V bytes from the epoch start (the ADD payload's head)
 			const uint32_t side = lane >> 5, w = (lane >> 2) & 7u, part = lane & 3u;
 			const uint32_t bytes = src.rd4(side, (side ? r0 : v0) + w + 4 * part);
 			uint64_t lo = 0, hi = 0;
@@ -823,7 +826,14 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
 		if (nrec >= rec_cap) { st = 7; break; }
-		if (lane < 3) rec[3u * nrec + lane] = lane == 0 ? vm : (lane == 1 ? rm : ml);
+		if constexpr (!Src::kPhaseA) {   // HBM-direct source: the payload word from V
+			if (vm > v0) {
+				uint32_t w = 0;
+				for (uint32_t k = 0; k < 4 && v0 + k < vl; ++k) w |= (uint32_t)src.V[v0 + k] << (8 * k);
+				pw = w;
+			}
+		}
+		if (lane < 4) rec[kRecWordsOnepass * nrec + lane] = lane == 0 ? vm : (lane == 1 ? rm : (lane == 2 ? ml : pw));
 		++nrec;
 		dsz += 13 + (vm > v0 ? 9 + (uint64_t)(vm - v0) : 0);
 		v0 = vm + ml;
@@ -893,7 +903,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 			vm_drain();   // this wave's record stores have landed
 			__builtin_amdgcn_s_waitcnt(0xc07f);
 			st = serialize_wave<2 * kWinStride - 32>(a.out + off, res.dsz, a.ver + pd.v_off, (uint32_t)pd.v_len,
-			                                         a.rec + 3ull * pp.rec_base, res.nrec, (sw_lds8*)win);
+			                                         a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base, kRecWordsOnepass,
+			                                         res.nrec, (sw_lds8*)win);
 		}
 		if (lane == 0 && st != res.st) a.status[pair] = st;
 	}

@@ -78,7 +78,8 @@ __device__ __forceinline__ void be32_store(P o, uint32_t x) {
 template <int kCmd, typename P>
 __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint32_t my, uint32_t prev0,
                                          const uint32_t (&cv)[kCmd], const uint32_t (&cr)[kCmd],
-                                         const uint32_t (&cl)[kCmd], const uint8_t* V) {
+                                         const uint32_t (&cl)[kCmd], const uint32_t (&cw)[kCmd], bool inl,
+                                         const uint8_t* V) {
 	const uint32_t lane = lane_id();
 	uint32_t prev = prev0, o = my;
 	bool big[kCmd];
@@ -94,7 +95,9 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 				q[0] = 2;
 				be32_store(q + 1, prev);
 				be32_store(q + 5, gap);
-				if (gap <= 32) {
+				if (inl && gap <= 4) {   // payload carried in the record
+					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = (uint8_t)(cw[i] >> (8 * k));
+				} else if (gap <= 32) {
 					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = V[prev + k];
 				} else {
 					big[i] = true;
@@ -130,7 +133,8 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 // disagree with `size`.
 template <uint32_t kStageBytes, int kCmd = 1>
 __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint8_t* V, uint32_t vl,
-                                         const uint32_t* rec, uint32_t n, sw_lds8* stage) {
+                                         const uint32_t* rec, uint32_t W, uint32_t n, sw_lds8* stage) {
+	const bool inl = W >= 4;   // 4th record word: V bytes from the gap start
 	const uint32_t lane = lane_id();
 	if (lane == 0) {
 		out[0] = 'D'; out[1] = 'L'; out[2] = 'T'; out[3] = 3;
@@ -141,20 +145,21 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 	uint32_t prev_end = 0;   // end of the previous tile's last COPY
 	// the next tile's records are loaded while this tile is assembled: their
 	// latency hides under this tile's payload loads
-	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd];
+	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd], ncw[kCmd];
 #pragma unroll
 	for (int i = 0; i < kCmd; ++i) {
 		const uint32_t j = kCmd * lane + i;
-		ncv[i] = ncr[i] = ncl[i] = 0;
+		ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
 		if (j < n) {
-			ncv[i] = rec[3u * j];
-			ncr[i] = rec[3u * j + 1];
-			ncl[i] = rec[3u * j + 2];
+			ncv[i] = rec[W * j];
+			ncr[i] = rec[W * j + 1];
+			ncl[i] = rec[W * j + 2];
+			if (inl) ncw[i] = rec[W * j + 3];
 		}
 	}
 	for (uint32_t t0 = 0; t0 < n; t0 += 64 * kCmd) {
 		bool valid[kCmd];
-		uint32_t cv[kCmd], cr[kCmd], cl[kCmd];
+		uint32_t cv[kCmd], cr[kCmd], cl[kCmd], cw[kCmd];
 #pragma unroll
 		for (int i = 0; i < kCmd; ++i) {
 			const uint32_t j = t0 + kCmd * lane + i;
@@ -162,12 +167,14 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			cv[i] = ncv[i];
 			cr[i] = ncr[i];
 			cl[i] = ncl[i];
+			cw[i] = ncw[i];
 			const uint32_t jn = j + 64 * kCmd;
-			ncv[i] = ncr[i] = ncl[i] = 0;
+			ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
 			if (jn < n) {
-				ncv[i] = rec[3u * jn];
-				ncr[i] = rec[3u * jn + 1];
-				ncl[i] = rec[3u * jn + 2];
+				ncv[i] = rec[W * jn];
+				ncr[i] = rec[W * jn + 1];
+				ncl[i] = rec[W * jn + 2];
+				if (inl) ncw[i] = rec[W * jn + 3];
 			}
 		}
 		// the lane's last valid command end, and the lane's byte count
@@ -198,7 +205,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 		const uint32_t my = incl - sz;
 		const uint32_t S = rdlane(incl, 63);
 		if (S <= kStageBytes) {
-			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, V);
+			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, cw, inl, V);
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // staged bytes are in LDS
 			__builtin_amdgcn_wave_barrier();
 			// flush: head bytes to a dword boundary, dwords, tail bytes
@@ -220,7 +227,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // LDS reads done before the next tile
 			__builtin_amdgcn_wave_barrier();
 		} else {
-			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, V);
+			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, cw, inl, V);
 		}
 		pos += S;
 		prev_end = rdlane(last, 63);
