@@ -667,18 +667,184 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 	return x;
 }
 
-__global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
+// ── decode: one 256-thread block (4 waves) per delta stream ──
+//
+// Per window: all four waves build N1..N8; wave 0 walks; all expand.  The
+// window's commands are then applied 64 per wave at a time, all four waves
+// at once, when the window is provably order-free: destinations increasing
+// and disjoint in stream order and no in-place COPY that moves (src == dst
+// in-place copies are no-ops).  Any other window is applied by wave 0 alone,
+// batch by batch, with the conflict check and the strict memmove replay.
+// The block barrier between windows also orders every store of one window
+// before the next window's reads and writes.
+constexpr uint32_t kDecBlock = 256;
+constexpr uint32_t kDecWaves = kDecBlock / 64;
+
+struct DecCmd {
+	bool mine;
+	uint32_t kind;
+	uint64_t src, dst, len;
+};
+
+template <typename WP>
+__device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b, uint32_t cnt, uint64_t pos) {
+	DecCmd c{false, 0, 0, 0, 0};
+	const uint32_t lane = lane_id();
+	c.mine = b + lane < cnt;
+	if (c.mine) {
+		const uint32_t cx = cmds[b + lane];
+		c.kind = w[cx];
+		if (c.kind == 1) {
+			c.src = be32(w + cx + 1);
+			c.dst = be32(w + cx + 5);
+			c.len = be32(w + cx + 9);
+		} else {
+			c.src = pos + cx + 9;   // payload offset in the stream
+			c.dst = be32(w + cx + 1);
+			c.len = be32(w + cx + 5);
+		}
+	}
+	return c;
+}
+
+// Per-wave LDS scratch of the flat copy.
+struct DecScratch {
+	uint32_t* cum;        // [64] byte prefix per non-empty command
+	uint32_t* row;        // [128] row start masks (lo dwords, then hi dwords)
+	const uint8_t** sp;   // [64]
+	uint8_t** dp;         // [64]
+};
+
+// Copy an independent batch (no command overlaps another one's writes, or
+// in-place, reads): byte j of the batch's concatenation goes to lane j % 64
+// in row j / 64; the owning command comes from per-row start masks (owner =
+// starts before the row + popcount(mask bits <= lane) - 1).  Branch-free per
+// row: owners and addresses, then the loads, then the predicated stores.
+// In-place COPYs whose source and destination overlap are memmoved after.
+__device__ void dec_flat_batch(const DecCmd& c, bool inplace, uint8_t* O, const uint8_t* R, const uint8_t* D,
+                               const DecScratch& x) {
+	const uint32_t lane = lane_id();
+	const uint8_t* sp = c.kind == 1 ? (inplace ? O + c.src : R + c.src) : D + c.src;
+	const bool selfov = c.mine && c.kind == 1 && inplace && c.src != c.dst && overlap(c.src, c.len, c.dst, c.len);
+	const bool noop = c.mine && c.kind == 1 && inplace && c.src == c.dst;
+	const uint32_t flen = (c.mine && !selfov && !noop) ? (uint32_t)c.len : 0u;
+	const uint32_t incl = dec_incl_scan(flen);
+	const uint32_t cum = incl - flen;
+	const uint32_t total = rdlane(incl, 63);
+	const bool nz = flen != 0;
+	const uint32_t ord = dec_incl_scan(nz ? 1u : 0u) - 1u;
+	if (nz) {
+		x.cum[ord] = cum;
+		x.sp[ord] = sp;
+		x.dp[ord] = O + c.dst;
+	}
+	typedef __attribute__((address_space(1))) const uint8_t gcu8;
+	typedef __attribute__((address_space(1))) uint8_t gu8;
+	for (uint32_t r0 = 0; 64 * r0 < total; r0 += 64) {   // 64 rows = 4 KiB per round
+		x.row[lane] = 0;
+		x.row[64 + lane] = 0;
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		if (nz && cum >= 64 * r0 && cum < 64 * (r0 + 64)) {
+			const uint32_t row = cum / 64 - r0, bit = cum % 64;
+			atomicOr(&x.row[(bit >> 5) * 64 + row], 1u << (bit & 31));
+		}
+		const uint32_t carry = (uint32_t)__builtin_popcountll(__ballot(nz && cum < 64 * r0));
+		__builtin_amdgcn_s_waitcnt(0xc07f);
+		__builtin_amdgcn_wave_barrier();
+		const uint64_t mrow = ((uint64_t)x.row[64 + lane] << 32) | x.row[lane];   // row r0 + lane
+		const uint32_t pc = (uint32_t)__builtin_popcountll(mrow);
+		const uint32_t rbase = carry + dec_incl_scan(pc) - pc;   // starts before row r0 + lane
+		const uint32_t nrows = min(64u, (total + 63) / 64 - r0);
+		constexpr int kQ = 16;   // rows per pass (VGPR budget: 4 waves per SIMD)
+		for (uint32_t q0 = 0; q0 < nrows; q0 += kQ) {
+			gu8* da[kQ];
+			uint8_t v[kQ];
+			bool ok[kQ];
+#pragma unroll
+			for (int uu = 0; uu < kQ; ++uu) {
+				const uint32_t u = q0 + uu;
+				const uint32_t j = 64 * (r0 + u) + lane;
+				ok[uu] = u < nrows && j < total;
+				const uint64_t m = ((uint64_t)rdlane((uint32_t)(mrow >> 32), u) << 32) | rdlane((uint32_t)mrow, u);
+				const uint32_t oo = rdlane(rbase, u) + (uint32_t)__builtin_popcountll(m & mask_le(lane));
+				const uint32_t o = ok[uu] && oo ? oo - 1u : 0u;
+				const uint32_t off = j - x.cum[o];
+				gcu8* sa = ok[uu] ? (gcu8*)(x.sp[o] + off) : (gcu8*)D;   // invalid rows read a harmless byte
+				da[uu] = (gu8*)(x.dp[o] + off);
+				v[uu] = *sa;
+			}
+#pragma unroll
+			for (int uu = 0; uu < kQ; ++uu)
+				if (ok[uu]) *da[uu] = v[uu];
+		}
+	}
+	for (uint64_t m = __ballot(selfov); m; m &= m - 1) {
+		const uint32_t kk = ffs64(m);
+		const uint64_t ks = ((uint64_t)rdlane((uint32_t)(c.src >> 32), kk) << 32) | rdlane((uint32_t)c.src, kk);
+		const uint64_t kd = ((uint64_t)rdlane((uint32_t)(c.dst >> 32), kk) << 32) | rdlane((uint32_t)c.dst, kk);
+		const uint64_t kl = ((uint64_t)rdlane((uint32_t)(c.len >> 32), kk) << 32) | rdlane((uint32_t)c.len, kk);
+		wave_memmove(O + kd, O + ks, kl);
+	}
+}
+
+// One batch in stream order (wave 0 of a window that is not order-free):
+// conflict check among the batch's commands, then the flat copy or the
+// strict memmove replay (apply.c:257-266), then a full wait.
+__device__ void dec_ordered_batch(const DecCmd& c, uint32_t n, bool inplace, uint8_t* O, const uint8_t* R,
+                                  const uint8_t* D, const DecScratch& x) {
+	const uint32_t lane = lane_id();
+	bool conflict = false;
+	const bool reads_buf = inplace && c.kind == 1;
+	for (uint32_t k = 0; k + 1 < n; ++k) {
+		const uint64_t ks = ((uint64_t)rdlane((uint32_t)(c.src >> 32), k) << 32) | rdlane((uint32_t)c.src, k);
+		const uint64_t kd = ((uint64_t)rdlane((uint32_t)(c.dst >> 32), k) << 32) | rdlane((uint32_t)c.dst, k);
+		const uint64_t kl = ((uint64_t)rdlane((uint32_t)(c.len >> 32), k) << 32) | rdlane((uint32_t)c.len, k);
+		const bool kreads = inplace && rdlane(c.kind, k) == 1;
+		if (c.mine && lane > k) {
+			if (overlap(kd, kl, c.dst, c.len)) conflict = true;
+			if (reads_buf && overlap(kd, kl, c.src, c.len)) conflict = true;
+			if (kreads && overlap(ks, kl, c.dst, c.len)) conflict = true;
+		}
+	}
+	if (__ballot(conflict) == 0) {
+		dec_flat_batch(c, inplace, O, R, D, x);
+	} else {
+		for (uint32_t k = 0; k < n; ++k) {
+			const uint32_t kk = rdlane(c.kind, k);
+			const uint64_t ks = ((uint64_t)rdlane((uint32_t)(c.src >> 32), k) << 32) | rdlane((uint32_t)c.src, k);
+			const uint64_t kd = ((uint64_t)rdlane((uint32_t)(c.dst >> 32), k) << 32) | rdlane((uint32_t)c.dst, k);
+			const uint64_t kl = ((uint64_t)rdlane((uint32_t)(c.len >> 32), k) << 32) | rdlane((uint32_t)c.len, k);
+			wave_memmove(O + kd, kk == 1 ? (inplace ? O + ks : R + ks) : D + ks, kl);
+		}
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void decode_kernel(DecodeArgs a) {
 	const uint32_t i = blockIdx.x;
 	if (i >= a.n) return;
-	const uint32_t lane = lane_id();
+	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
 	__shared__ __attribute__((aligned(16))) uint8_t win[kDecWin + 32];
-	__shared__ uint16_t N1[kDecWin], N2[kDecWin], N4[kDecWin], N8[kDecWin];
+	__shared__ uint16_t N1[kDecWin];
+	// N2, N4, N8 during the parse; the waves' flat-copy scratch afterwards
+	__shared__ __attribute__((aligned(16))) uint16_t NX[3 * kDecWin];
 	__shared__ uint16_t cmds[kDecMaxCmds];
 	__shared__ uint16_t jumps[kDecMaxCmds / 8 + 1];
-	__shared__ uint32_t c_cum[64];               // flat copy, per non-empty command: byte prefix,
-	__shared__ uint32_t c_row[128];              // row start masks (lo dwords, then hi dwords)
-	__shared__ const uint8_t* c_sp[64];          // source and
-	__shared__ uint8_t* c_dp[64];                // destination
+	__shared__ uint32_t sh[8];   // walk results and window flags
+	uint16_t* N2 = NX;
+	uint16_t* N4 = NX + kDecWin;
+	uint16_t* N8 = NX + 2 * kDecWin;
+	static_assert(kDecWaves * (64 * 4 + 128 * 4 + 64 * 8 + 64 * 8) <= 3 * kDecWin * 2, "scratch fits NX");
+	DecScratch xs;
+	{
+		uint8_t* base = reinterpret_cast<uint8_t*>(NX) + wave * (64 * 4 + 128 * 4 + 64 * 8 + 64 * 8);
+		xs.sp = reinterpret_cast<const uint8_t**>(base);
+		xs.dp = reinterpret_cast<uint8_t**>(base + 64 * 8);
+		xs.cum = reinterpret_cast<uint32_t*>(base + 128 * 8);
+		xs.row = reinterpret_cast<uint32_t*>(base + 128 * 8 + 64 * 4);
+	}
 
 #ifdef DG_ONEPASS_PROF
 	uint64_t dprof[kDecProfN] = {};
@@ -702,7 +868,7 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	const uint64_t bsz = inplace ? max(rl, vsize) : vsize;
 	if (!st && bsz > dd.out_cap) st = 7;
 	if (st) {
-		if (lane == 0) {
+		if (tid == 0) {
 			a.status[i] = st;
 			a.out_len[i] = 0;
 			if (a.out_spans) a.out_spans[i].len = 0;
@@ -714,60 +880,55 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 	DPROF_T(tf0);
 	{
 		uint64_t k0 = 0;
-		if ((((uintptr_t)O | (uintptr_t)R) & 15) == 0) {   // 16 B per lane, 4 in flight
+		if ((((uintptr_t)O | (uintptr_t)R) & 15) == 0) {   // 16 B per thread, 4 in flight
 			const uint64_t n16 = init / 16;
-			for (uint64_t b = 0; b < n16; b += 256) {
+			for (uint64_t b = 0; b < n16; b += 4 * kDecBlock) {
 				uint4 x[4];
 #pragma unroll
 				for (int u = 0; u < 4; ++u) {
-					const uint64_t q = b + 64 * u + lane;
+					const uint64_t q = b + kDecBlock * u + tid;
 					if (q < n16) x[u] = reinterpret_cast<const uint4*>(R)[q];
 				}
 #pragma unroll
 				for (int u = 0; u < 4; ++u) {
-					const uint64_t q = b + 64 * u + lane;
+					const uint64_t q = b + kDecBlock * u + tid;
 					if (q < n16) reinterpret_cast<uint4*>(O)[q] = x[u];
 				}
 			}
 			const uint64_t z0 = (init + 15) / 16, z1 = bsz / 16;   // whole zero words [z0, z1)
-			for (uint64_t q = z0 + lane; q < z1; q += 64) reinterpret_cast<uint4*>(O)[q] = make_uint4(0, 0, 0, 0);
-			for (uint64_t k = n16 * 16 + lane; k < z0 * 16 && k < bsz; k += 64) O[k] = k < init ? R[k] : 0;
+			for (uint64_t q = z0 + tid; q < z1; q += kDecBlock) reinterpret_cast<uint4*>(O)[q] = make_uint4(0, 0, 0, 0);
+			for (uint64_t k = n16 * 16 + tid; k < z0 * 16 && k < bsz; k += kDecBlock) O[k] = k < init ? R[k] : 0;
 			k0 = (z1 > z0 ? z1 : z0) * 16;
 		}
-		for (uint64_t k = k0 + lane; k < bsz; k += 64) O[k] = k < init ? R[k] : 0;
+		for (uint64_t k = k0 + tid; k < bsz; k += kDecBlock) O[k] = k < init ? R[k] : 0;
 	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__builtin_amdgcn_wave_barrier();
+	__syncthreads();   // every wave's image stores complete before any command store
 	DPROF_ADD(DP_FILL, tf0);
 
 	uint64_t pos = 25;   // stream offset of the current window: a command boundary
 	bool done = false;
-	uint32_t hwm = 0;    // end of the highest destination written while every batch stayed ordered
 	while (!done && !st) {
 		if (pos >= dl) break;   // missing END: end of input (as the reference's loop)
 		const uint32_t avail = (uint32_t)min((uint64_t)kDecWin, dl - pos);
 		// ── 1. window -> LDS: aligned 16-byte blocks that hold stream bytes
 		//    (a block never crosses a page), win[sh + x] = D[pos + x]
 		const uintptr_t wa = (uintptr_t)(D + pos) & ~(uintptr_t)15;
-		const uint32_t sh = (uint32_t)((uintptr_t)(D + pos) - wa);
+		const uint32_t shf = (uint32_t)((uintptr_t)(D + pos) - wa);
 		const uintptr_t dend = (uintptr_t)(D + dl);
 		DPROF_INC(DP_WINDOWS);
 		DPROF_T(tl0);
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		for (uint32_t q = lane; q < (kDecWin + 32) / 16; q += 64) {
+		for (uint32_t q = tid; q < (kDecWin + 32) / 16; q += kDecBlock) {
 			const uintptr_t ad = wa + 16 * q;
 			uint4 x = make_uint4(0, 0, 0, 0);
 			if (ad < dend) x = *reinterpret_cast<const uint4*>(ad);
 			reinterpret_cast<uint4*>(win)[q] = x;
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		const uint8_t* w = win + sh;
+		__syncthreads();
+		const uint8_t* w = win + shf;
 		DPROF_ADD(DP_LOAD, tl0);
 		DPROF_T(tn0);
 		// ── 2. N1: next command offset for a command starting at x ──
-		for (uint32_t x = lane; x < kDecWin; x += 64) {
+		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
 			uint16_t nx = kNxBad;
 			if (x < avail) {
 				const uint32_t t = w[x];
@@ -787,55 +948,63 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 			}
 			N1[x] = nx;
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
+		__syncthreads();
 		DPROF_ADD(DP_N1, tn0);
 		DPROF_T(td0);
 		// ── 3. pointer doubling ──
-		for (uint32_t x = lane; x < kDecWin; x += 64) {
+		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
 			const uint16_t y = N1[x];
 			N2[x] = y >= kNxSpecial ? y : N1[y];
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		for (uint32_t x = lane; x < kDecWin; x += 64) {
+		__syncthreads();
+		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
 			const uint16_t y = N2[x];
 			N4[x] = y >= kNxSpecial ? y : N2[y];
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		for (uint32_t x = lane; x < kDecWin; x += 64) {
+		__syncthreads();
+		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
 			const uint16_t y = N4[x];
 			N8[x] = y >= kNxSpecial ? y : N4[y];
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
+		__syncthreads();
 		DPROF_ADD(DP_DBL, td0);
 		DPROF_T(tw0);
-		// ── 4. the walk (uniform): 8 commands per N8 step, then single steps ──
-		uint32_t x = 0, nj = 0;
-		uint16_t term = 0;   // the code that ended the walk
-		while (true) {
-			const uint32_t y = uni(N8[x]);
-			if (y >= kNxSpecial || 8 * (nj + 1) > kDecMaxCmds) break;
-			if (lane == 0) jumps[nj] = (uint16_t)x;
-			++nj;
-			x = y;
+		// ── 4. the walk (wave 0, uniform): 8 commands per N8 step, then single steps ──
+		if (wave == 0) {
+			uint32_t x = 0, nj = 0;
+			uint32_t term = 0;
+			while (true) {
+				const uint32_t y = uni(N8[x]);
+				if (y >= kNxSpecial || 8 * (nj + 1) > kDecMaxCmds) break;
+				if (lane == 0) jumps[nj] = (uint16_t)x;
+				++nj;
+				x = y;
+			}
+			uint32_t cnt = 8 * nj;
+			while (true) {   // single steps from x (at most 7 commands + the terminal)
+				const uint32_t y = uni(N1[x]);
+				if (y == kNxEnd || y == kNxBad || y == kNxCut) { term = y; break; }
+				if (cnt >= kDecMaxCmds) { term = kNxCut; break; }   // restart the window at x
+				if (lane == 0) cmds[cnt] = (uint16_t)x;
+				++cnt;
+				if (y == kNxFar) { term = kNxFar; break; }
+				x = y;
+			}
+			if (lane == 0) {
+				sh[0] = cnt;
+				sh[1] = nj;
+				sh[2] = x;
+				sh[3] = term;
+				sh[4] = 0;   // a batch out of bounds
+				sh[5] = 0;   // the window is not order-free
+			}
 		}
-		uint32_t cnt = 8 * nj;
-		while (true) {   // single steps from x (at most 7 commands + the terminal)
-			const uint32_t y = uni(N1[x]);
-			if (y == kNxEnd || y == kNxBad || y == kNxCut) { term = (uint16_t)y; break; }
-			if (cnt >= kDecMaxCmds) { term = kNxCut; break; }   // restart the window at x
-			if (lane == 0) cmds[cnt] = (uint16_t)x;
-			++cnt;
-			if (y == kNxFar) { term = kNxFar; break; }
-			x = y;
-		}
+		__syncthreads();
+		const uint32_t cnt = sh[0], nj = sh[1], x = sh[2], term = sh[3];
 		DPROF_ADD(DP_WALK, tw0);
 		DPROF_T(te0);
 		// expand the jumps: the 8 nodes from jumps[j]
-		for (uint32_t j = lane; j < nj; j += 64) {
+		for (uint32_t j = tid; j < nj; j += kDecBlock) {
 			const uint32_t e0 = jumps[j];
 			const uint32_t e2 = N2[e0], e4 = N4[e0];
 			const uint32_t e6 = N2[e4];
@@ -849,8 +1018,7 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 			c[6] = (uint16_t)e6;
 			c[7] = N1[e6];
 		}
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
+		__syncthreads();   // cmds complete; N2..N8 dead: NX becomes the copy scratch
 		DPROF_ADD(DP_EXP, te0);
 		// the walk's terminal: x is where it stopped
 		uint64_t next_pos = pos + x;   // kNxCut: restart at x
@@ -860,158 +1028,55 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 			const uint32_t t = w[x];
 			next_pos = pos + x + (t == 1 ? 13u : 9u + be32(w + x + 5));
 		}
-		if (term == kNxCut && cnt == 0 && x == 0) st = 8;   // cannot happen: a header fits 4 KiB
 
-		// ── 5. apply the window's commands, 64 at a time ──
-		for (uint32_t b = 0; b < cnt && !st; b += 64) {
-			DPROF_INC(DP_BATCHES);
-			DPROF_T(th0);
-			const bool mine = b + lane < cnt;
-			uint32_t kind = 0;
-			uint64_t src = 0, dst = 0, len = 0;
-			if (mine) {
-				const uint32_t cx = cmds[b + lane];
-				kind = w[cx];
-				if (kind == 1) {
-					src = be32(w + cx + 1);
-					dst = be32(w + cx + 5);
-					len = be32(w + cx + 9);
-				} else {
-					src = pos + cx + 9;   // payload offset in the stream
-					dst = be32(w + cx + 1);
-					len = be32(w + cx + 5);
-				}
-			}
+		// ── 5. bounds and order checks of every batch (waves in parallel) ──
+		DPROF_T(th0);
+		const uint32_t nb = (cnt + 63) / 64;
+		for (uint32_t b = wave; b < nb; b += kDecWaves) {
+			const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
 			bool bad = false;
-			if (mine) {
-				if (dst + len > bsz) bad = true;
-				if (kind == 1 && src + len > (inplace ? bsz : rl)) bad = true;
+			if (c.mine) {
+				if (c.dst + c.len > bsz) bad = true;
+				if (c.kind == 1 && c.src + c.len > (inplace ? bsz : rl)) bad = true;
 			}
-			if (__ballot(bad)) { st = 8; break; }
-			// conflicts among the batch's commands (writes vs writes; and
-			// in-place: writes vs reads both ways).  Fast proof: destinations
-			// in increasing, disjoint order and no in-place COPY that moves.
-			const uint32_t end32 = (uint32_t)(dst + len), dst32 = (uint32_t)dst;   // < 2^32 (bsz checked)
+			// order-free: destinations increasing and disjoint (< 2^32: bsz
+			// checked) and no in-place COPY that moves
+			const uint32_t end32 = (uint32_t)(c.dst + c.len), dst32 = (uint32_t)c.dst;
 			uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end32, 0x138, 0xF, 0xF, false);
-			const bool unordered = mine && ((lane > 0 && dst32 < prev_end) || (lane == 0 && dst32 < hwm));
-			const bool moves = mine && inplace && kind == 1 && src != dst;
-			// ordered after everything applied so far: no wait needed before
-			// the next batch (no byte written twice, no buffer byte read)
-			const bool after_all = __ballot(unordered || moves) == 0;
-			bool conflict = false;
-			if (!after_all) {
-				// earlier batches may still have stores in flight that this one
-				// reads or overwrites
-				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-				__builtin_amdgcn_wave_barrier();
-				const bool reads_buf = inplace && kind == 1;
-				const uint32_t n = cnt - b < 64 ? cnt - b : 64;
-				for (uint32_t k = 0; k + 1 < n; ++k) {
-					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), k) << 32) | rdlane((uint32_t)src, k);
-					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), k) << 32) | rdlane((uint32_t)dst, k);
-					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), k) << 32) | rdlane((uint32_t)len, k);
-					const bool kreads = inplace && rdlane(kind, k) == 1;
-					if (mine && lane > k) {
-						if (overlap(kd, kl, dst, len)) conflict = true;
-						if (reads_buf && overlap(kd, kl, src, len)) conflict = true;
-						if (kreads && overlap(ks, kl, dst, len)) conflict = true;
-					}
-				}
+			if (lane == 0 && b > 0) {   // the last command of the batch before
+				const DecCmd p = dec_cmd(w, cmds, 64 * b - 1, cnt, pos);
+				prev_end = (uint32_t)(p.dst + p.len);
 			}
-			DPROF_ADD(DP_HDR, th0);
-			DPROF_T(tc0);
-			if (__ballot(conflict) == 0) {
-				// Independent commands.  An in-place COPY whose source and
-				// destination overlap keeps its memmove (src == dst is a no-op).
-				// Every other byte of the batch is copied in one flat pass: byte
-				// j of the batch's concatenation goes to lane j % 64, with 16
-				// loads per lane in flight before their stores.
-				const uint8_t* sp = kind == 1 ? (inplace ? O + src : R + src) : D + src;
-				const bool selfov = mine && kind == 1 && inplace && src != dst && overlap(src, len, dst, len);
-				const bool noop = mine && kind == 1 && inplace && src == dst;
-				const uint32_t flen = (mine && !selfov && !noop) ? (uint32_t)len : 0u;
-				// Element j of the batch's byte concatenation is done by lane
-				// j % 64 in row j / 64.  The command owning j is found without a
-				// walk: rows carry a 64-bit mask of where non-empty commands
-				// start, so owner = (starts before the row) + popcount(mask
-				// bits <= lane) - 1, an ordinal into the non-empty commands.
-				const uint32_t incl = dec_incl_scan(flen);
-				const uint32_t cum = incl - flen;
-				const uint32_t total = rdlane(incl, 63);
-				const bool nz = flen != 0;
-				const uint32_t ord = dec_incl_scan(nz ? 1u : 0u) - 1u;
-				if (nz) {
-					c_cum[ord] = cum;
-					c_sp[ord] = sp;
-					c_dp[ord] = O + dst;
+			const bool unordered = c.mine && (lane > 0 || b > 0) && dst32 < prev_end;
+			const bool moves = c.mine && inplace && c.kind == 1 && c.src != c.dst;
+			if (__ballot(bad) && lane == 0) atomicOr(&sh[4], 1u);
+			if (__ballot(unordered || moves) && lane == 0) atomicOr(&sh[5], 1u);
+		}
+		__syncthreads();
+		if (sh[4]) st = 8;
+		DPROF_ADD(DP_HDR, th0);
+		DPROF_T(tc0);
+		// ── 6. apply ──
+		if (!st) {
+			if (!sh[5]) {
+				for (uint32_t b = wave; b < nb; b += kDecWaves) {
+					DPROF_INC(DP_BATCHES);
+					const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
+					dec_flat_batch(c, inplace, O, R, D, xs);
 				}
-				typedef __attribute__((address_space(1))) const uint8_t gcu8;
-				typedef __attribute__((address_space(1))) uint8_t gu8;
-				for (uint32_t r0 = 0; 64 * r0 < total; r0 += 64) {   // 64 rows = 4 KiB per round
-					// start masks of rows r0 .. r0+63 (LDS, as two dwords per row)
-					c_row[lane] = 0;
-					c_row[64 + lane] = 0;
-					__builtin_amdgcn_s_waitcnt(0xc07f);
-					__builtin_amdgcn_wave_barrier();
-					if (nz && cum >= 64 * r0 && cum < 64 * (r0 + 64)) {
-						const uint32_t row = cum / 64 - r0, bit = cum % 64;
-						atomicOr(&c_row[(bit >> 5) * 64 + row], 1u << (bit & 31));
-					}
-					const uint32_t carry = (uint32_t)__builtin_popcountll(__ballot(nz && cum < 64 * r0));
-					__builtin_amdgcn_s_waitcnt(0xc07f);
-					__builtin_amdgcn_wave_barrier();
-					const uint64_t mrow = ((uint64_t)c_row[64 + lane] << 32) | c_row[lane];   // row r0 + lane
-					const uint32_t pc = (uint32_t)__builtin_popcountll(mrow);
-					const uint32_t rbase = carry + dec_incl_scan(pc) - pc;   // starts before row r0 + lane
-					const uint32_t nrows = min(64u, (total + 63) / 64 - r0);
-					uint32_t o[64];
-					uint8_t v[64];
-#pragma unroll
-					for (int u = 0; u < 64; ++u) {
-						const uint32_t j = 64 * (r0 + u) + lane;
-						o[u] = 0xFFFFFFFFu;
-						if ((uint32_t)u < nrows && j < total) {
-							const uint64_t m = ((uint64_t)rdlane((uint32_t)(mrow >> 32), u) << 32) | rdlane((uint32_t)mrow, u);
-							o[u] = rdlane(rbase, u) + (uint32_t)__builtin_popcountll(m & mask_le(lane)) - 1u;
-							v[u] = *(gcu8*)(c_sp[o[u]] + (j - c_cum[o[u]]));
-						}
-					}
-#pragma unroll
-					for (int u = 0; u < 64; ++u) {
-						const uint32_t j = 64 * (r0 + u) + lane;
-						if (o[u] != 0xFFFFFFFFu) *(gu8*)(c_dp[o[u]] + (j - c_cum[o[u]])) = v[u];
-					}
+			} else if (wave == 0) {
+				for (uint32_t b = 0; b < nb; ++b) {
+					DPROF_INC(DP_BATCHES);
+					const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
+					dec_ordered_batch(c, cnt - 64 * b < 64 ? cnt - 64 * b : 64, inplace, O, R, D, xs);
 				}
-				for (uint64_t m = __ballot(selfov); m; m &= m - 1) {
-					const uint32_t kk = ffs64(m);
-					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), kk) << 32) | rdlane((uint32_t)src, kk);
-					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), kk) << 32) | rdlane((uint32_t)dst, kk);
-					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), kk) << 32) | rdlane((uint32_t)len, kk);
-					wave_memmove(O + kd, O + ks, kl);
-				}
-			} else {
-				// strict stream order (apply.c:257-266)
-				const uint32_t n = cnt - b < 64 ? cnt - b : 64;
-				for (uint32_t k = 0; k < n; ++k) {
-					const uint32_t kk = rdlane(kind, k);
-					const uint64_t ks = ((uint64_t)rdlane((uint32_t)(src >> 32), k) << 32) | rdlane((uint32_t)src, k);
-					const uint64_t kd = ((uint64_t)rdlane((uint32_t)(dst >> 32), k) << 32) | rdlane((uint32_t)dst, k);
-					const uint64_t kl = ((uint64_t)rdlane((uint32_t)(len >> 32), k) << 32) | rdlane((uint32_t)len, k);
-					wave_memmove(O + kd, kk == 1 ? (inplace ? O + ks : R + ks) : D + ks, kl);
-				}
-			}
-			DPROF_ADD(DP_COPY, tc0);
-			if (after_all) {
-				hwm = uni(wave_max_u32(mine ? end32 : 0u)) > hwm ? uni(wave_max_u32(mine ? end32 : 0u)) : hwm;
-			} else {
-				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-				__builtin_amdgcn_wave_barrier();
-				hwm = 0xFFFFFFFFu;   // order unknown from here: every later batch waits
 			}
 		}
+		__syncthreads();   // the window's stores complete before the next window
+		DPROF_ADD(DP_COPY, tc0);
 		pos = next_pos;
 	}
-	if (lane == 0) {
+	if (tid == 0) {
 		a.status[i] = st;
 		a.out_len[i] = st ? 0 : vsize;
 		if (a.out_spans) a.out_spans[i].len = st ? 0 : vsize;
@@ -1022,7 +1087,7 @@ __global__ __launch_bounds__(64) void decode_kernel(DecodeArgs a) {
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		DPROF_ADD(DP_WAIT, tw9);
 		dprof[DP_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
-		if (lane == 0)
+		if (tid == 0)
 			for (int k = 0; k < kDecProfN; ++k) atomicAdd(&g_decode_prof[k], (unsigned long long)dprof[k]);
 	}
 #endif
@@ -1051,7 +1116,7 @@ __global__ __launch_bounds__(64) void decode_verify_kernel(const uint8_t* delta,
 }
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
-	if (a.n) hipLaunchKernelGGL(decode_kernel, dim3(a.n), dim3(64), 0, st, a);
+	if (a.n) hipLaunchKernelGGL(decode_kernel, dim3(a.n), dim3(kDecBlock), 0, st, a);
 	return hipGetLastError();
 }
 

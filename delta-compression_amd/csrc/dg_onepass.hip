@@ -82,6 +82,17 @@ __device__ unsigned long long g_onepass_prof[kProfN];
 #define PROF_ADD(o, i, v) ((void)0)
 #endif
 
+#ifdef DG_REFILL_PROF   // variant build: refill-wait cycles, refills, pair cycles
+__device__ unsigned long long g_refill_prof[3];
+extern "C" int dg_refill_prof_read(unsigned long long* out) {
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refill_prof), 24) == hipSuccess ? 0 : -1;
+}
+extern "C" int dg_refill_prof_reset(void) {
+	unsigned long long z[3] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_refill_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // ───────────────────────────── small helpers ──────────────────────────────
 
 __device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -236,6 +247,10 @@ struct WinSrc {
 	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
 	const uint64_t* powc;
 	PROF_DECL
+#ifdef DG_REFILL_PROF
+	uint64_t refill_cycles = 0;
+	uint32_t refill_count = 0;
+#endif
 
 	// (re)load whichever window does not cover [lo, lo+need); both streams'
 	// LDS-DMA requests are in flight before the single wait
@@ -272,8 +287,15 @@ struct WinSrc {
 			}
 			base[1] = nb;
 		}
+#ifdef DG_REFILL_PROF
+		const uint64_t tr0 = __builtin_amdgcn_s_memtime();
+#endif
 		vm_drain();        // the DMA landed (ordered by vmcnt) ...
 		__syncthreads();   // ... and is visible to every lane
+#ifdef DG_REFILL_PROF
+		refill_cycles += __builtin_amdgcn_s_memtime() - tr0;
+		++refill_count;
+#endif
 		PROF_ADD(*this, P_REFILLS, 1);
 		PROF_ADD(*this, P_T_REFILL, PROF_NOW_R() - t0);
 	}
@@ -887,7 +909,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	const uint32_t part = lane_id() & 3u;
 #pragma unroll
 	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
+#ifdef DG_REFILL_PROF
+	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
+#endif
 	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+#ifdef DG_REFILL_PROF
+	if (lane_id() == 0) {
+		atomicAdd(&g_refill_prof[0], (unsigned long long)src.refill_cycles);
+		atomicAdd(&g_refill_prof[1], (unsigned long long)src.refill_count);
+		atomicAdd(&g_refill_prof[2], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_all0));
+	}
+#endif
 	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
 	if (a.lookback) {
 		// fused placement + serialisation (dg_serialize_wave.h)
