@@ -343,13 +343,16 @@ struct WinSrc {
 	// one that fails the check are committed.  Returns the number committed;
 	// *adv = offset of the new state, *more = the batch ended only because the
 	// chain left the known region (another batch can follow directly),
-	// *dsz_add = their delta bytes.
+	// *dsz_add = their delta bytes, *long_first = nothing was committed
+	// because the first epoch's diagonal step is past 63 (phase A cannot
+	// resolve it on the diagonal: the caller starts phase B at step 0).
 	__device__ uint32_t diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
 	                               uint64_t qmag, uint32_t p, uint32_t* rec, uint32_t nrec,
 	                               uint32_t rec_cap, uint32_t* mlist, uint32_t* adv, bool* more,
-	                               uint32_t* dsz_add) {
+	                               uint32_t* dsz_add, bool* long_first) {
 		const uint32_t lane = lane_id();
 		const uint32_t lim = umin32(vl - v0, rl - r0);
+		*long_first = false;
 		*adv = 0;
 		*more = false;
 		*dsz_add = 0;
@@ -399,7 +402,10 @@ struct WinSrc {
 		const bool cand = gap && lane < kb;        // members, in chain order
 		const uint32_t Bend = wave_incl_scan(cand ? T + 1 : 0u);   // steps through this member
 		uint64_t left = __ballot(cand);
-		if (!left) return 0;
+		if (!left) {
+			*long_first = tooLong != 0;
+			return 0;
+		}
 		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
 		// Members are taken in rounds of at most 64 steps (a member never
 		// straddles two rounds); the first member that fails its check ends
@@ -620,17 +626,20 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	uint32_t v0 = 0, r0 = 0;
 	bool scanning = vl > 0;
 	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
+	bool skipA = false;         // the epoch is known to be long: phase B from step 0
 	while (scanning) {
+		skipA = false;
 		// no match is possible once either stream cannot supply a window at
 		// the epoch start (the reference keeps scanning the other, :102-104)
 		if (v0 + p > vl || r0 + p > rl) break;
 		if constexpr (Src::kPhaseA) {
 			if (at_mismatch) {
 				uint32_t adv = 0, dadd = 0;
-				bool more = false;
+				bool more = false, lf = false;
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
 				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, p, rec, nrec, rec_cap, bm,
-				                                      &adv, &more, &dadd));
+				                                      &adv, &more, &dadd, &lf));
+				skipA = f == 0 && uni((uint32_t)lf);
 				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
 				PROF_ADD(src, P_DIAG_CALLS, 1);
 				PROF_ADD(src, P_DIAG_EPOCHS, f);
@@ -655,7 +664,11 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		uint32_t pw = 0;   // 4th record word
 
 		// ── phase A: steps 0..7, four lanes per window ──
-		if constexpr (Src::kPhaseA) {
+		if constexpr (Src::kPhaseA) if (skipA) {
+			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
+			pw = uni(src.rd4(0, v0));   // V bytes from the epoch start (the ADD payload's head)
+		}
+		if constexpr (Src::kPhaseA) if (!skipA) {
 			[[maybe_unused]] const uint64_t ta = PROF_NOW();
 			PROF_ADD(src, P_A_ENTRIES, 1);
 			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
@@ -743,7 +756,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				const bool p2 = cv && ((bm[64 + ((sV >> 5) & 63u)] >> (sV & 31u)) & 1u);
 				const uint64_t m1 = __ballot(p1), m2 = __ballot(p2);
 				// steps phase A already ruled out are skipped
-				const uint32_t j0 = (Src::kPhaseA && c == 0) ? 8u : 0u;
+				const uint32_t j0 = (Src::kPhaseA && c == 0 && !skipA) ? 8u : 0u;
 				uint64_t walk = (m1 | m2) & ~((1ull << j0) - 1ull);
 				if constexpr (Src::kPhaseA) PROF_ADD(src, P_B_WALKED, __builtin_popcountll(walk));
 				while (walk) {
