@@ -212,6 +212,7 @@ __device__ __forceinline__ uint32_t tab_lookup(unsigned long long* t, uint32_t s
 template <int PF>
 struct GlobalSrc {
 	static constexpr bool kPhaseA = false;
+	static constexpr uint32_t kBmWords = 64;   // phase-B bitmap: 2048 bits per table
 	const uint8_t* V;
 	const uint8_t* R;
 	uint32_t p;
@@ -241,6 +242,7 @@ constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
 struct WinSrc {
 	static constexpr bool kPhaseA = true;
+	static constexpr uint32_t kBmWords = 128;  // phase-B bitmap: 4096 bits per table (bm[256])
 	const uint8_t* S[2];     // V, R (16-byte aligned)
 	uint32_t len[2];
 	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
@@ -745,15 +747,19 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				// so far, per table.  A step whose slot misses the other
 				// table's bitmap has no candidate at all; only the remaining
 				// steps are walked exactly (in step order).
-				if (c == 0) { bm[lane] = 0u; bm[64 + lane] = 0u; }
+				constexpr uint32_t BW = Src::kBmWords;   // bitmap words per table
+				if (c == 0) {
+#pragma unroll
+					for (uint32_t k = 0; k < 2 * BW; k += 64) bm[k + lane] = 0u;
+				}
 				__builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
 				__builtin_amdgcn_wave_barrier();
-				if (cv) atomicOr(&bm[(sV >> 5) & 63u], 1u << (sV & 31u));
-				if (cr) atomicOr(&bm[64 + ((sR >> 5) & 63u)], 1u << (sR & 31u));
+				if (cv) atomicOr(&bm[(sV >> 5) & (BW - 1u)], 1u << (sV & 31u));
+				if (cr) atomicOr(&bm[BW + ((sR >> 5) & (BW - 1u))], 1u << (sR & 31u));
 				__builtin_amdgcn_s_waitcnt(0xc07f);
 				__builtin_amdgcn_wave_barrier();
-				const bool p1 = cr && ((bm[(sR >> 5) & 63u] >> (sR & 31u)) & 1u);
-				const bool p2 = cv && ((bm[64 + ((sV >> 5) & 63u)] >> (sV & 31u)) & 1u);
+				const bool p1 = cr && ((bm[(sR >> 5) & (BW - 1u)] >> (sR & 31u)) & 1u);
+				const bool p2 = cv && ((bm[BW + ((sV >> 5) & (BW - 1u))] >> (sV & 31u)) & 1u);
 				const uint64_t m1 = __ballot(p1), m2 = __ballot(p2);
 				// steps phase A already ruled out are skipped
 				const uint32_t j0 = (Src::kPhaseA && c == 0 && !skipA) ? 8u : 0u;
