@@ -79,7 +79,7 @@ template <int kCmd, typename P>
 __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint32_t my, uint32_t prev0,
                                          const uint32_t (&cv)[kCmd], const uint32_t (&cr)[kCmd],
                                          const uint32_t (&cl)[kCmd], const uint32_t (&cw)[kCmd], bool inl,
-                                         const uint8_t* V) {
+                                         const uint8_t* V, uint32_t vl) {
 	const uint32_t lane = lane_id();
 	uint32_t prev = prev0, o = my;
 	bool big[kCmd];
@@ -98,7 +98,25 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 				if (inl && gap <= 4) {   // payload carried in the record
 					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = (uint8_t)(cw[i] >> (8 * k));
 				} else if (gap <= 32) {
-					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = V[prev + k];
+					// up to 8 (unaligned) dword loads in flight instead of a
+					// chain of byte loads; never past the end of V
+					uint32_t wd[8];
+#pragma unroll
+					for (int k = 0; k < 8; ++k) {
+						const uint32_t o4 = 4u * k;
+						wd[k] = 0;
+						if (o4 < gap) {
+							if (prev + o4 + 4 <= vl) {
+								__builtin_memcpy(&wd[k], V + prev + o4, 4);
+							} else {
+								for (uint32_t b = 0; b < 4 && prev + o4 + b < vl; ++b)
+									wd[k] |= (uint32_t)V[prev + o4 + b] << (8 * b);
+							}
+						}
+					}
+#pragma unroll
+					for (int k = 0; k < 32; ++k)
+						if ((uint32_t)k < gap) q[9 + k] = (uint8_t)(wd[k >> 2] >> (8 * (k & 3)));
 				} else {
 					big[i] = true;
 					bsrc[i] = prev;
@@ -116,12 +134,24 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 			prev = cv[i] + cl[i];
 		}
 	}
+	// long payloads: the whole wave, 4 bytes per lane per pass (unaligned
+	// dword loads, never past the end of V)
 #pragma unroll
 	for (int i = 0; i < kCmd; ++i)
 		for (uint64_t bm = __ballot(big[i]); bm; bm &= bm - 1) {
 			const uint32_t k = ffs64(bm);
 			const uint32_t src = rdlane(bsrc[i], k), len = rdlane(blen[i], k), dst = rdlane(bdst[i], k);
-			for (uint32_t x = lane; x < len; x += 64) base[dst + x] = V[src + x];
+			for (uint32_t x = 4 * lane; x < len; x += 256) {
+				uint32_t w = 0;
+				if (src + x + 4 <= vl) {
+					__builtin_memcpy(&w, V + src + x, 4);
+				} else {
+					for (uint32_t b = 0; b < 4 && src + x + b < vl; ++b) w |= (uint32_t)V[src + x + b] << (8 * b);
+				}
+#pragma unroll
+				for (uint32_t b = 0; b < 4; ++b)
+					if (x + b < len) base[dst + x + b] = (uint8_t)(w >> (8 * b));
+			}
 		}
 }
 
@@ -205,7 +235,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 		const uint32_t my = incl - sz;
 		const uint32_t S = rdlane(incl, 63);
 		if (S <= kStageBytes) {
-			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, cw, inl, V);
+			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, cw, inl, V, vl);
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // staged bytes are in LDS
 			__builtin_amdgcn_wave_barrier();
 			// flush: head bytes to a dword boundary, dwords, tail bytes
@@ -227,7 +257,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // LDS reads done before the next tile
 			__builtin_amdgcn_wave_barrier();
 		} else {
-			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, cw, inl, V);
+			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, cw, inl, V, vl);
 		}
 		pos += S;
 		prev_end = rdlane(last, 63);
