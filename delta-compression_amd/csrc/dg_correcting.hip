@@ -39,6 +39,7 @@ constexpr uint32_t kBuildSeedsPerLane = 16;
 constexpr uint32_t kBuildBlock = 256;
 constexpr uint32_t kBuildSeedsPerBlock = kBuildSeedsPerLane * kBuildBlock;   // 4096
 
+
 __device__ __forceinline__ uint32_t umin_(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
 __device__ __forceinline__ uint64_t fold61c(uint64_t lo, uint64_t hi) {
@@ -174,9 +175,17 @@ __device__ uint32_t ext_bwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
 
 // ───────────────────────────── build ──────────────────────────────────────
 
+// checkpoint class of every pair, one thread per pair (the p-byte Horner
+// chain is serial; computing it once here keeps it off the build blocks)
+__global__ __launch_bounds__(64) void correcting_class_kernel(EncodeArgs a) {
+	const uint32_t pair = blockIdx.x * 64 + threadIdx.x;
+	if (pair >= a.n_pairs) return;
+	const PairDev pd = a.pairs[pair];
+	a.kcls[pair] = checkpoint_class(a.ver + pd.v_off, pd.v_len, a.p, a.pplan[pair]);
+}
+
 __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a) {
 	__shared__ uint64_t ob[256];   // x * 263^(p-1) mod M: the byte leaving the window
-	__shared__ uint64_t kcls;
 	const uint32_t pair = blockIdx.x;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
@@ -190,14 +199,48 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 		const uint32_t x = threadIdx.x;
 		ob[x] = fold61c((uint64_t)x * (uint32_t)top, (uint64_t)x * (uint32_t)(top >> 32));
 	}
-	if (threadIdx.x == 0) kcls = checkpoint_class(a.ver + pd.v_off, pd.v_len, p, pp);
 	__syncthreads();
-	const uint64_t k = kcls;
+	const uint64_t k = a.kcls[pair];
 	uint32_t* H = a.ctab + pp.tab_base;
 
 	const uint64_t s0 = blk0 + (uint64_t)threadIdx.x * kBuildSeedsPerLane;
 	if (s0 >= seeds) return;
 	const uint32_t cnt = (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane);
+	if (p == 16 && cnt == kBuildSeedsPerLane) {
+		// the lane's 31 bytes R[s0 .. s0+31) in two (unaligned) 16-byte loads;
+		// s0 + 31 <= |R| here, and the 32nd byte is read only if it exists
+		uint32_t w[8];
+		__builtin_memcpy(w, R + s0, 16);
+		if (s0 + 32 <= pd.r_len) {
+			__builtin_memcpy(w + 4, R + s0 + 16, 16);
+		} else {
+			__builtin_memcpy(w + 4, R + s0 + 16, 12);
+			w[7] = (uint32_t)R[s0 + 28] | ((uint32_t)R[s0 + 29] << 8) | ((uint32_t)R[s0 + 30] << 16);
+		}
+		auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+		uint64_t fp = 0;
+		{
+			uint64_t lo = 0, hi = 0;
+#pragma unroll
+			for (int kk = 0; kk < 16; ++kk) {
+				const uint64_t c = a.powc[kk];
+				const uint64_t b = byte_at(kk);
+				lo += b * (uint32_t)c;
+				hi += b * (uint32_t)(c >> 32);
+			}
+			fp = fold61c(lo, hi);
+		}
+#pragma unroll
+		for (uint32_t j = 0; j < kBuildSeedsPerLane; ++j) {
+			if (j) {   // roll (hash.c:62-98)
+				const uint64_t t = mod_m61(fp + kMersenne - ob[byte_at(j - 1)]);
+				fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 15), (t >> 32) * (uint32_t)kBase);
+			}
+			uint32_t slot;
+			if (checkpoint_slot(fp, pp, k, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
+		}
+		return;
+	}
 	uint64_t fp = window_fp<0>(R + s0, p, a.powc);
 	for (uint32_t j = 0; j < cnt; ++j) {
 		if (j) {   // roll: (fp - R[a-1] * 263^(p-1)) * 263 + R[a-1+p]   (hash.c:62-98)
@@ -264,7 +307,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 	};
 
 	if (vl > 0) {
-		const uint64_t k = uni64(checkpoint_class(V, vl, p, pp));
+		const uint64_t k = uni64(a.kcls[pair]);
 		uint32_t vc = 0, vs = 0;
 		while (st == 0 && vc + p <= vl) {
 			// ── positions vc .. vc+63: fingerprint, checkpoint, lookup, memcmp ──
@@ -351,6 +394,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st) {
 	(void)p;
 	if (a.n_pairs == 0) return hipSuccess;
+	hipLaunchKernelGGL(correcting_class_kernel, dim3((a.n_pairs + 63) / 64), dim3(64), 0, st, a);
 	if (a.max_seeds) {
 		const dim3 grid(a.n_pairs, (a.max_seeds + kBuildSeedsPerBlock - 1) / kBuildSeedsPerBlock);
 		hipLaunchKernelGGL(correcting_build_kernel, grid, dim3(kBuildBlock), 0, st, a);

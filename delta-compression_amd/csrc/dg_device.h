@@ -86,6 +86,7 @@ struct EncodeArgs {
 	uint32_t buf_cap;          // lookback buffer entries (correcting.c:14-62)
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
+	uint64_t* kcls;            // per pair: checkpoint class k (correcting.c:131-136), computed once
 	uint32_t wave_prio;        // onepass16: s_setprio level (issue priority over the CRC waves)
 	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
 };

@@ -296,7 +296,7 @@ struct dg_encode_plan {
 	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
-	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback;
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
@@ -456,7 +456,10 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_tables.alloc(per * P->n_tables);
 	bad |= P->d_locks.alloc(4ull * P->n_tables);
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
-	if (algo == DG_ALGO_CORRECTING) bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
+	if (algo == DG_ALGO_CORRECTING) {
+		bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
+		bad |= P->d_kcls.alloc(8ull * std::max<uint32_t>(n, 1));
+	}
 	{
 		// DG_FUSED=1: onepass16 serialises in-kernel behind a decoupled look-back.
 		// Off by default: the look-back couples every wave to the slowest pair
@@ -637,6 +640,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		} else {
 			// fresh R indexes (~0 = empty slot), then build + scan
 			a.ctab = P->d_ctab.as<uint32_t>();
+			a.kcls = P->d_kcls.as<uint64_t>();
 			a.max_seeds = (uint32_t)P->max_seeds;
 			HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
 			HIPCHK(ctx, launch_correcting(a, a.p, st));

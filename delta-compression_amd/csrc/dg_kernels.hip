@@ -315,8 +315,9 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	__syncthreads();
 	const uint32_t wave = threadIdx.x >> 6;
 	const uint32_t lane = lane_id();
-	const uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave;
-	if (seg >= a.n_segs) return;
+	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
+	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
+	     seg += gridDim.x * kCrcWavesPerBlock) {
 	const CrcSegDev sd = a.segs[seg];
 	const CrcSpanDev sp = a.spans[sd.span];
 	const uintptr_t start = (uintptr_t)(a.arena[sp.which] + sp.off);
@@ -370,6 +371,7 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
 	}
 	if (lane == 0) a.seg_crc[seg] = reg;
+	}
 }
 
 __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
@@ -538,10 +540,15 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 }
 
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st) {
-	if (a.n_segs)
-		hipLaunchKernelGGL(crc_segments_kernel,
-		                   dim3((a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock),
-		                   dim3(64 * kCrcWavesPerBlock), 0, st, a);
+	if (a.n_segs) {
+		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
+		static const uint32_t cap = [] {   // DG_CRC_BLOCKS: cap the grid (A/B of the CRC's footprint)
+			const char* e = getenv("DG_CRC_BLOCKS");
+			return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+		}();
+		if (cap && blocks > cap) blocks = cap;
+		hipLaunchKernelGGL(crc_segments_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
 	return hipGetLastError();
