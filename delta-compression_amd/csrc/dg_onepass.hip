@@ -109,6 +109,10 @@ __device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
 	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
 }
+// same shift, lane 0 receives 0 (bound_ctrl: one instruction, no old value)
+__device__ __forceinline__ uint32_t wave_shr1z(uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, true);
+}
 // inclusive prefix sum over the wave: row_shr 1/2/4/8 inside rows of 16, then
 // row_bcast:15 / row_bcast:31 across rows (all DPP, no LDS round trips)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -180,6 +184,21 @@ __device__ __forceinline__ uint64_t fold61(uint64_t lo, uint64_t hi) {
 	return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
 }
 
+// Bit 8j + g -> bit 4g + j (j < 4, g < 8): the 5-bit index (j1 j0 g2 g1 g0)
+// becomes (g2 g1 g0 j1 j0), a rotation done as index-bit swaps (delta swaps).
+__device__ __forceinline__ uint32_t delta_swap(uint32_t x, uint32_t mask, uint32_t sh) {
+	const uint32_t t = ((x >> sh) ^ x) & mask;
+	return x ^ t ^ (t << sh);
+}
+__device__ __forceinline__ uint32_t mask_transpose_8x4(uint32_t x) {
+	// the index-bit 5-cycle 0->2->4->1->3->0 as the swaps (0 2)(0 4)(0 1)(0 3)
+	x = delta_swap(x, 0x0A0A0A0Au, 3);
+	x = delta_swap(x, 0x0000AAAAu, 15);
+	x = delta_swap(x, 0x22222222u, 1);
+	x = delta_swap(x, 0x00AA00AAu, 7);
+	return x;
+}
+
 // ───────────────────────────── table tier ─────────────────────────────────
 
 __device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
@@ -236,7 +255,10 @@ struct GlobalSrc {
 #endif
 constexpr uint32_t kWin = DG_WIN_BYTES;     // bytes per stream window (3 KiB: 7.2 KiB LDS per wave, 5 waves/SIMD)
 constexpr uint32_t kLook = DG_LOOK_BYTES;   // diagonal batch: lookahead bytes per lane
-constexpr uint32_t kShortT = 12;            // look-back by DPP shifts up to this epoch length
+#ifndef DG_SHORT_T
+#define DG_SHORT_T 32
+#endif
+constexpr uint32_t kShortT = DG_SHORT_T;    // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
@@ -363,13 +385,18 @@ struct WinSrc {
 		ensure2(v0, r0, 64 * kLook + 48, true, true);
 		// 1. mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
 		const uint32_t base = kLook * lane;
+		// byte j of word g first lands at bit 8j + g (one shift-and-or per
+		// word), then a 5-bit index rotation (four delta swaps) moves it to
+		// bit 4g + j, i.e. offset order
+		static_assert(kLook == 32, "one 32-bit mismatch mask per lane");
 		uint32_t bits = 0;
 #pragma unroll
-		for (uint32_t g = 0; g < kLook / 4; ++g) {
+		for (uint32_t g = 0; g < 8; ++g) {
 			const uint32_t x = rd4(0, v0 + base + 4 * g) ^ rd4(1, r0 + base + 4 * g);
-			const uint32_t t = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;   // byte != 0
-			bits |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * g);
+			const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
+			bits |= (t >> (7 - g)) & (0x01010101u << g);
 		}
+		bits = mask_transpose_8x4(bits);
 		if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
 			bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
 			if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
@@ -463,7 +490,29 @@ struct WinSrc {
 			//    wave shifts; the largest matching d is the earliest writer,
 			//    whose fingerprint rides along.
 			uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
-			if (maxT <= kShortT) {
+			if (maxT <= kShortT && q < (1ull << 25)) {
+				// Keys tag each slot with its member (slot + 1 | j << 25), so
+				// a shifted key can only equal a lane's own key when it comes
+				// from the same member: no per-shift range test, and the
+				// fingerprints are fetched once for the final candidates.
+				const uint32_t kv = live ? ((sV + 1u) | (j << 25)) : 0xFFFFFFFFu;
+				const uint32_t kr = live ? ((sR + 1u) | (j << 25)) : 0xFFFFFFFEu;
+				uint32_t d1 = kv == kr ? 0u : 0xFFu;   // largest shift with a match
+				uint32_t d2 = d1;
+				uint32_t xv = kv, xr = kr;
+#pragma unroll
+				for (uint32_t d = 1; d <= kShortT; ++d) {
+					if (d > maxT) break;
+					xv = wave_shr1z(xv);
+					xr = wave_shr1z(xr);
+					d1 = xv == kr ? d : d1;
+					d2 = xr == kv ? d : d2;
+				}
+				s1 = d1 != 0xFFu ? lane - d1 : 64u;
+				s2 = d2 != 0xFFu ? lane - d2 : 64u;
+				f1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s1 << 2), (int)fVl);
+				f2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s2 << 2), (int)fRl);
+			} else if (maxT <= kShortT) {
 				uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
 				for (uint32_t d = 0; d <= maxT; ++d) {
 					if (d) {
