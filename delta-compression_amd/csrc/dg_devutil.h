@@ -37,6 +37,42 @@ __device__ __forceinline__ uint64_t mod_q(uint64_t x, uint64_t q, uint64_t magic
 	return r;
 }
 
+// x mod q for q < 2^25 in FP64 (full-rate FMA on CDNA; the 64-bit Barrett
+// above needs four quarter-rate 32x32 multiplies).  x = xh 2^32 + xl:
+//   r1 = xh - floor(xh / q) q        (== xh mod q up to one q either way)
+//   y  = r1 (2^32 mod q) + xl        (|y| < 2^52: exact)
+//   r  = y - floor(y / q) q          (in [-q, 2q), exact)
+// and two unsigned minimums bring r into [0, q).  The quotients are off by at
+// most one because |quotient| * 2^-52 < 1.
+struct ModQ {
+	double qd, inv, k1;   // q, 1/q, 2^32 mod q
+	bool ok;              // q < 2^25: this path applies
+};
+
+__device__ __forceinline__ ModQ make_modq(uint64_t q, uint64_t magic) {
+	ModQ m;
+	m.ok = q < (1ull << 25);
+	m.qd = (double)q;
+	m.inv = 1.0 / m.qd;
+	m.k1 = (double)mod_q(1ull << 32, q, magic);
+	return m;
+}
+
+__device__ __forceinline__ uint32_t mod_q_small(uint64_t x, const ModQ& m) {
+	const double xh = (double)(uint32_t)(x >> 32), xl = (double)(uint32_t)x;
+	const double r1 = __fma_rn(-floor(xh * m.inv), m.qd, xh);
+	const double y = __fma_rn(r1, m.k1, xl);
+	const uint32_t u = (uint32_t)(int32_t)__fma_rn(-floor(y * m.inv), m.qd, y);
+	const uint32_t q = (uint32_t)m.qd;
+	const uint32_t v = min(u, u + q);
+	return min(v, v - q);
+}
+
+// slot = x mod q by whichever path applies (m.ok is wave-uniform)
+__device__ __forceinline__ uint32_t slot_of(uint64_t x, const ModQ& m, uint64_t q, uint64_t magic) {
+	return m.ok ? mod_q_small(x, m) : (uint32_t)mod_q(x, q, magic);
+}
+
 // Karp-Rabin fingerprint of d[0..p) (src/c/hash.c:28-38) as a dot product
 // with the constants powc[k] = 263^(p-1-k) mod M: each term is an 8-bit x
 // 61-bit product, split into 32-bit halves so that both partial sums fit in

@@ -371,7 +371,7 @@ struct WinSrc {
 	// because the first epoch's diagonal step is past 63 (phase A cannot
 	// resolve it on the diagonal: the caller starts phase B at step 0).
 	__device__ uint32_t diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
-	                               uint64_t qmag, uint32_t p, uint32_t* rec, uint32_t nrec,
+	                               uint64_t qmag, const ModQ& mq, uint32_t p, uint32_t* rec, uint32_t nrec,
 	                               uint32_t rec_cap, uint32_t* mlist, uint32_t* adv, bool* more,
 	                               uint32_t* dsz_add, bool* long_first) {
 		const uint32_t lane = lane_id();
@@ -478,8 +478,8 @@ struct WinSrc {
 			PROF_ADD(*this, P_T_D3A, PROF_NOW() - tq);
 			if (live) {
 				const uint64_t fV = fp16(0, v0 + js + t), fR = fp16(1, r0 + js + t);
-				sV = (uint32_t)mod_q(fV, q, qmag);
-				sR = (uint32_t)mod_q(fR, q, qmag);
+				sV = slot_of(fV, mq, q, qmag);
+				sR = slot_of(fR, mq, q, qmag);
 				fVl = (uint32_t)fV;
 				fRl = (uint32_t)fR;
 			}
@@ -662,6 +662,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	const uint32_t lane = lane_id();
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
+	const ModQ mq = make_modq(q, qmag);
 	const uint32_t rec_cap = uni(pp.rec_cap);
 	uint32_t* __restrict__ rec = a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base;
 
@@ -688,7 +689,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				uint32_t adv = 0, dadd = 0;
 				bool more = false, lf = false;
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
-				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, p, rec, nrec, rec_cap, bm,
+				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm,
 				                                      &adv, &more, &dadd, &lf));
 				skipA = f == 0 && uni((uint32_t)lf);
 				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
@@ -735,7 +736,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			}
 			const uint64_t fp = fold61(quad_sum64(lo), quad_sum64(hi));
 			const bool valid = w < (side ? nr : nv);
-			const uint32_t slot = valid ? (uint32_t)mod_q(fp, q, qmag) : kSentinel;
+			const uint32_t slot = valid ? slot_of(fp, mq, q, qmag) : kSentinel;
 			const uint32_t fpl = (uint32_t)fp;
 			const uint32_t tA = umin32(8u, nlive);
 			for (uint32_t t = 0; t < tA; ++t) {
@@ -783,8 +784,8 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 			uint64_t fV = 0, fR = 0;
 			uint32_t sV = kSentinel, sR = kSentinel;
-			if (cv) { fV = src.fpV(v0 + step); sV = (uint32_t)mod_q(fV, q, qmag); }
-			if (cr) { fR = src.fpR(r0 + step); sR = (uint32_t)mod_q(fR, q, qmag); }
+			if (cv) { fV = src.fpV(v0 + step); sV = slot_of(fV, mq, q, qmag); }
+			if (cr) { fR = src.fpR(r0 + step); sR = slot_of(fR, mq, q, qmag); }
 			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
 
 			if constexpr (Src::kPhaseA) PROF_ADD(src, c < (uint32_t)kHistChunks ? P_B_CHUNKS : P_C_CHUNKS, 1);
