@@ -333,6 +333,29 @@ struct WinSrc {
 		return __builtin_amdgcn_alignbyte(w1, w0, i & 3u);
 	}
 
+	// the 8 words at stream offset x .. x+31 (x - window base: the same value
+	// mod 16 in every lane)
+	template <uint32_t Q>
+	__device__ __forceinline__ static void pick8(const uint32_t (&d)[12], uint32_t r, uint32_t (&w)[8]) {
+#pragma unroll
+		for (uint32_t k = 0; k < 8; ++k) w[k] = __builtin_amdgcn_alignbyte(d[Q + k + 1], d[Q + k], r);
+	}
+	__device__ __forceinline__ void lane_words32(uint32_t s, uint32_t x, uint32_t (&w)[8]) const {
+		const uint32_t i = x - (s ? base[1] : base[0]);
+		typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+		typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+		const lds_u32x4* p = (const lds_u32x4*)(win + (s ? kWinStride : 0) + (i & ~15u));
+		const u32x4 a = p[0], b = p[1], c = p[2];
+		const uint32_t d[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+		const uint32_t o = uni(i & 15u), r = o & 3u;
+		switch (o >> 2) {
+		case 0: pick8<0>(d, r, w); break;
+		case 1: pick8<1>(d, r, w); break;
+		case 2: pick8<2>(d, r, w); break;
+		default: pick8<3>(d, r, w); break;
+		}
+	}
+
 	__device__ __forceinline__ uint64_t fp16(uint32_t s, uint32_t x) const {
 		return fp16_dot(rd4(s, x), rd4(s, x + 4), rd4(s, x + 8), rd4(s, x + 12));
 	}
@@ -364,35 +387,42 @@ struct WinSrc {
 	//                  with lookup 2 then finding s = T_k.
 	// "Earliest s" is the reference's first-writer slot (HV/HR hold the first
 	// step of the epoch that hashed to the slot).  The epochs before the first
-	// one that fails the check are committed.  Returns the number committed;
-	// *adv = offset of the new state, *more = the batch ended only because the
-	// chain left the known region (another batch can follow directly),
-	// *dsz_add = their delta bytes, *long_first = nothing was committed
-	// because the first epoch's diagonal step is past 63 (phase A cannot
-	// resolve it on the diagonal: the caller starts phase B at step 0).
-	__device__ uint32_t diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
-	                               uint64_t qmag, const ModQ& mq, uint32_t p, uint32_t* rec, uint32_t nrec,
-	                               uint32_t rec_cap, uint32_t* mlist, uint32_t* adv, bool* more,
-	                               uint32_t* dsz_add, bool* long_first) {
+	// one that fails the check are committed.  Returns (all wave-uniform, by
+	// value so nothing goes through scratch): the number committed, adv =
+	// offset of the new state, more = the batch ended only because the chain
+	// left the known region (another batch can follow directly), dadd = their
+	// delta bytes, long_first = nothing was committed because the first
+	// epoch's diagonal step is past 63 (phase A cannot resolve it on the
+	// diagonal: the caller starts phase B at step 0).
+	struct DiagOut {
+		uint32_t committed, adv, more, dadd, long_first;
+	};
+	__device__ DiagOut diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
+	                              uint64_t qmag, const ModQ& mq, uint32_t p, uint32_t* rec, uint32_t nrec,
+	                              uint32_t rec_cap, uint32_t* mlist) {
 		const uint32_t lane = lane_id();
 		const uint32_t lim = umin32(vl - v0, rl - r0);
-		*long_first = false;
-		*adv = 0;
-		*more = false;
-		*dsz_add = 0;
-		if (lim < p + 1) return 0;
+		if (lim < p + 1) return DiagOut{0, 0, 0, 0, 0};
 		[[maybe_unused]] uint64_t tq = PROF_NOW();
 		ensure2(v0, r0, 64 * kLook + 48, true, true);
 		// 1. mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
 		const uint32_t base = kLook * lane;
+		// The lane's 32 bytes of each stream come in as three ds_read_b128 from
+		// the 16-byte-aligned address below them (2-way bank conflicts; word
+		// reads at a 32-byte lane stride are 8-way).  The offset inside the
+		// 16 bytes is wave-uniform (windows and lane chunks are 16-aligned),
+		// so picking the 8 words is a uniform switch plus alignbytes.
+		static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
+		uint32_t wv[8], wr[8];
+		lane_words32(0, v0 + base, wv);
+		lane_words32(1, r0 + base, wr);
 		// byte j of word g first lands at bit 8j + g (one shift-and-or per
 		// word), then a 5-bit index rotation (four delta swaps) moves it to
 		// bit 4g + j, i.e. offset order
-		static_assert(kLook == 32, "one 32-bit mismatch mask per lane");
 		uint32_t bits = 0;
 #pragma unroll
 		for (uint32_t g = 0; g < 8; ++g) {
-			const uint32_t x = rd4(0, v0 + base + 4 * g) ^ rd4(1, r0 + base + 4 * g);
+			const uint32_t x = wv[g] ^ wr[g];
 			const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
 			bits |= (t >> (7 - g)) & (0x01010101u << g);
 		}
@@ -410,7 +440,7 @@ struct WinSrc {
 		__builtin_amdgcn_s_waitcnt(0xc07f);
 		__builtin_amdgcn_wave_barrier();
 		const uint32_t K = umin32(total, 64u);
-		if (K < 2) return 0;
+		if (K < 2) return DiagOut{0, 0, 0, 0, 0};
 		PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
 		tq = PROF_NOW();
 		const uint32_t ak = lane < K ? mlist[lane] : 0xFFFFFFFFu;
@@ -431,10 +461,7 @@ struct WinSrc {
 		const bool cand = gap && lane < kb;        // members, in chain order
 		const uint32_t Bend = wave_incl_scan(cand ? T + 1 : 0u);   // steps through this member
 		uint64_t left = __ballot(cand);
-		if (!left) {
-			*long_first = tooLong != 0;
-			return 0;
-		}
+		if (!left) return DiagOut{0, 0, 0, 0, tooLong != 0 ? 1u : 0u};
 		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
 		// Members are taken in rounds of at most 64 steps (a member never
 		// straddles two rounds); the first member that fails its check ends
@@ -616,10 +643,7 @@ struct WinSrc {
 			rbase = rdlane(Bend, klast);
 			left &= ~VM;
 		}
-		*adv = advance;
-		*dsz_add = dadd;
-		*more = all;
-		return committed;
+		return DiagOut{committed, advance, all ? 1u : 0u, dadd, 0};
 	}
 
 	// wave-parallel forward extension (onepass.c:229-234), 256 B per pass
@@ -658,7 +682,7 @@ struct PairResult {
 template <class Src>
 __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
-                                             const uint64_t (&cA)[4], uint32_t* bm) {
+                                             uint32_t* bm) {
 	const uint32_t lane = lane_id();
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
@@ -686,23 +710,21 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		if (v0 + p > vl || r0 + p > rl) break;
 		if constexpr (Src::kPhaseA) {
 			if (at_mismatch) {
-				uint32_t adv = 0, dadd = 0;
-				bool more = false, lf = false;
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
-				const uint32_t f = uni(src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm,
-				                                      &adv, &more, &dadd, &lf));
-				skipA = f == 0 && uni((uint32_t)lf);
+				const auto dg = src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm);
+				const uint32_t f = uni(dg.committed);
+				skipA = f == 0 && uni(dg.long_first) != 0u;
 				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
 				PROF_ADD(src, P_DIAG_CALLS, 1);
 				PROF_ADD(src, P_DIAG_EPOCHS, f);
 				PROF_ADD(src, P_DIAG_ZERO, f == 0);
 				if (f) {
-					adv = uni(adv);
+					const uint32_t adv = uni(dg.adv);
 					nrec += f;
-					dsz += uni(dadd);
+					dsz += uni(dg.dadd);
 					v0 += adv;
 					r0 += adv;
-					if (uni((uint32_t)more)) continue;   // the chain left the region: next batch
+					if (uni(dg.more)) continue;   // the chain left the region: next batch
 					if (v0 + p > vl || r0 + p > rl) break;
 				}
 			}
@@ -729,10 +751,11 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			const uint32_t bytes = src.rd4(side, (side ? r0 : v0) + w + 4 * part);
 			uint64_t lo = 0, hi = 0;
 #pragma unroll
-			for (int j = 0; j < 4; ++j) {
+			for (int j = 0; j < 4; ++j) {   // constants 263^(15-k) for this lane's 4 bytes (L1-resident)
+				const uint64_t c = src.powc[4 * part + j];
 				const uint64_t b = (bytes >> (8 * j)) & 0xff;
-				lo += b * (uint32_t)cA[j];
-				hi += b * (uint32_t)(cA[j] >> 32);
+				lo += b * (uint32_t)c;
+				hi += b * (uint32_t)(c >> 32);
 			}
 			const uint64_t fp = fold61(quad_sum64(lo), quad_sum64(hi));
 			const bool valid = w < (side ? nr : nv);
@@ -974,14 +997,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	src.powc = a.powc;
 	PROF_INIT(src)
 	[[maybe_unused]] const uint64_t t_start = PROF_NOW_R();
-	uint64_t cA[4];
-	const uint32_t part = lane_id() & 3u;
-#pragma unroll
-	for (int j = 0; j < 4; ++j) cA[j] = a.powc[4 * part + j];
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
-	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, cA, bm);
+	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, bm);
 #ifdef DG_REFILL_PROF
 	if (lane_id() == 0) {
 		atomicAdd(&g_refill_prof[0], (unsigned long long)src.refill_cycles);
@@ -1023,8 +1042,7 @@ __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	GlobalSrc<PF> src{a.ver + pd.v_off, a.ref + pd.r_off, PF > 0 ? (uint32_t)PF : a.p, a.powc};
-	const uint64_t cA[4] = {0, 0, 0, 0};
-	onepass_pair(src, a, pair, pd, pp, src.p, cA, bm);
+	onepass_pair(src, a, pair, pd, pp, src.p, bm);
 }
 
 // DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B measurements)
