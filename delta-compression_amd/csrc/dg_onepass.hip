@@ -171,12 +171,20 @@ __device__ __forceinline__ uint64_t fp16_dot(uint32_t w0, uint32_t w1, uint32_t 
 			if (kFpLimb[j][g]) acc = __builtin_amdgcn_udot4(w[g], kFpLimb[j][g], acc, false);
 		D[j] = acc;
 	}
-	uint64_t x = (uint64_t)D[0] + ((uint64_t)D[1] << 8) + ((uint64_t)D[2] << 16) +
-	             ((uint64_t)D[3] << 24) + ((uint64_t)D[4] << 32) + ((uint64_t)D[5] << 40);
-	// 2^61 == 1 (mod M): fold what D_6, D_7 carry past bit 61
-	x += ((uint64_t)(D[6] & 0x1FFFu) << 48) + (D[6] >> 13);
-	x += ((uint64_t)(D[7] & 0x1Fu) << 56) + (D[7] >> 5);
-	return mod_m61(x);
+	// Combine in 32-bit pieces: P_i = D_2i + D_2i+1 2^8 < 2^29 and
+	//   fp = P0 + P1 2^16 + P2 2^32 + P3 2^48  (mod M),
+	// with P3 2^48 = (P3 & 0x1FFF) 2^48 + (P3 >> 13) 2^61 == ... + (P3 >> 13).
+	const uint32_t P0 = D[0] + (D[1] << 8), P1 = D[2] + (D[3] << 8);
+	const uint32_t P2 = D[4] + (D[5] << 8), P3 = D[6] + (D[7] << 8);
+	const uint32_t t = P0 + (P3 >> 13);                 // < 2^30
+	const uint32_t lo = t + (P1 << 16);
+	const uint32_t c = lo < t ? 1u : 0u;
+	const uint32_t hi = P2 + ((P3 & 0x1FFFu) << 16) + (P1 >> 16) + c;   // < 2^31
+	// x = hi 2^32 + lo < 2^63: one Mersenne fold and a final subtract
+	const uint32_t lo2 = lo + (hi >> 29);
+	const uint32_t hi2 = (hi & 0x1FFFFFFFu) + (lo2 < lo ? 1u : 0u);
+	uint64_t r = ((uint64_t)hi2 << 32) | lo2;            // <= 2^61 + 2
+	return r >= kMersenne ? r - kMersenne : r;
 }
 
 __device__ __forceinline__ uint64_t fold61(uint64_t lo, uint64_t hi) {
