@@ -159,7 +159,7 @@ hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block p
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st);
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
                                 const uint64_t* ref_crc, const uint64_t* out_crc, int32_t* status,

@@ -107,6 +107,7 @@ struct dg_context {
 	uint64_t* d_crc_tables = nullptr;   // slice(8x256) + levels(6x256)
 	uint64_t* d_xinv = nullptr;         // 16
 	uint64_t kseg = 0;
+	uint32_t n_cu = 256;                // compute units (grid caps)
 	std::string err;
 	// scratch reused by the host-buffer entry points
 	void* pin = nullptr;
@@ -183,6 +184,11 @@ int dg_context_create(int device, dg_context_t** out) {
 	ctx->device = device;
 	if (hipSetDevice(device) != hipSuccess) { delete ctx; return DG_ERR_HIP; }
 	if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return DG_ERR_HIP; }
+	{
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+			ctx->n_cu = (uint32_t)cus;
+	}
 
 	// CRC tables: slicing-by-8 and nibble tables of the combine constants
 	std::vector<uint64_t> tab(8 * 256 + kCrcLevels * kCrcNibTabWords);
@@ -601,7 +607,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
-		HIPCHK(ctx, launch_crc(a, cs));
+		HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu));
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[1], cs));
 		return DG_OK;
 	};
