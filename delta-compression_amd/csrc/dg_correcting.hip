@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dg_device.h"
 #include "dg_devutil.h"
 
@@ -35,9 +37,9 @@ namespace dg {
 namespace {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint32_t kBuildSeedsPerLane = 16;
+constexpr uint32_t kBuildSeedsPerLane = 32;
 constexpr uint32_t kBuildBlock = 256;
-constexpr uint32_t kBuildSeedsPerBlock = kBuildSeedsPerLane * kBuildBlock;   // 4096
+constexpr uint32_t kBuildSeedsPerBlock = kBuildSeedsPerLane * kBuildBlock;   // 8192
 
 
 __device__ __forceinline__ uint32_t umin_(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -184,14 +186,18 @@ __global__ __launch_bounds__(64) void correcting_class_kernel(EncodeArgs a) {
 	a.kcls[pair] = checkpoint_class(a.ver + pd.v_off, pd.v_len, a.p, a.pplan[pair]);
 }
 
-__global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a, uint32_t nchunk,
+                                                                       uint32_t lds_cap) {
 	__shared__ uint64_t ob[256];   // x * 263^(p-1) mod M: the byte leaving the window
-	const uint32_t pair = blockIdx.x;
-	const PairDev pd = a.pairs[pair];
+	const uint32_t xcd = blockIdx.x & 7u, i = blockIdx.x >> 3;
+	const uint32_t pair = (i / nchunk) * 8u + xcd, chunk = i % nchunk;
+	if (pair >= a.n_pairs) return;
 	const PairPlanDev pp = a.pplan[pair];
+	if (pp.q <= lds_cap) return;   // built in LDS by correcting_build_lds_kernel
+	const PairDev pd = a.pairs[pair];
 	const uint32_t p = a.p;
 	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
-	const uint64_t blk0 = (uint64_t)blockIdx.y * kBuildSeedsPerBlock;
+	const uint64_t blk0 = (uint64_t)chunk * kBuildSeedsPerBlock;
 	if (blk0 >= seeds || pd.v_len == 0) return;
 	const uint8_t* R = a.ref + pd.r_off;
 	const uint64_t top = a.powc[0];
@@ -202,34 +208,29 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 	__syncthreads();
 	const uint64_t k = a.kcls[pair];
 	uint32_t* H = a.ctab + pp.tab_base;
+	const Ckpt ck = make_ckpt(pp.f_size, pp.f_magic, pp.m, k, pp.q);
+	auto passes = [&](uint64_t fp, uint32_t* slot) -> bool {
+		return ck.mf.ok ? ckpt_test(fp, ck, slot) : checkpoint_slot(fp, pp, k, slot);
+	};
 
 	const uint64_t s0 = blk0 + (uint64_t)threadIdx.x * kBuildSeedsPerLane;
 	if (s0 >= seeds) return;
 	const uint32_t cnt = (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane);
 	if (p == 16 && cnt == kBuildSeedsPerLane) {
-		// the lane's 31 bytes R[s0 .. s0+31) in two (unaligned) 16-byte loads;
-		// s0 + 31 <= |R| here, and the 32nd byte is read only if it exists
-		uint32_t w[8];
-		__builtin_memcpy(w, R + s0, 16);
-		if (s0 + 32 <= pd.r_len) {
-			__builtin_memcpy(w + 4, R + s0 + 16, 16);
+		// the lane's 47 bytes R[s0 .. s0+47) in three (unaligned) 16-byte
+		// loads; s0 + 47 <= |R| here, and the 48th byte is read only if it
+		// exists
+		uint32_t w[12];
+		__builtin_memcpy(w, R + s0, 32);
+		if (s0 + 48 <= pd.r_len) {
+			__builtin_memcpy(w + 8, R + s0 + 32, 16);
 		} else {
-			__builtin_memcpy(w + 4, R + s0 + 16, 12);
-			w[7] = (uint32_t)R[s0 + 28] | ((uint32_t)R[s0 + 29] << 8) | ((uint32_t)R[s0 + 30] << 16);
+			__builtin_memcpy(w + 8, R + s0 + 32, 12);
+			w[11] = (uint32_t)R[s0 + 44] | ((uint32_t)R[s0 + 45] << 8) | ((uint32_t)R[s0 + 46] << 16);
 		}
 		auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
-		uint64_t fp = 0;
-		{
-			uint64_t lo = 0, hi = 0;
-#pragma unroll
-			for (int kk = 0; kk < 16; ++kk) {
-				const uint64_t c = a.powc[kk];
-				const uint64_t b = byte_at(kk);
-				lo += b * (uint32_t)c;
-				hi += b * (uint32_t)(c >> 32);
-			}
-			fp = fold61c(lo, hi);
-		}
+		// the first window by byte dot products, the rest by rolling
+		uint64_t fp = fp16_dot(w[0], w[1], w[2], w[3]);
 #pragma unroll
 		for (uint32_t j = 0; j < kBuildSeedsPerLane; ++j) {
 			if (j) {   // roll (hash.c:62-98)
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 				fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 15), (t >> 32) * (uint32_t)kBase);
 			}
 			uint32_t slot;
-			if (checkpoint_slot(fp, pp, k, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
+			if (passes(fp, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
 		}
 		return;
 	}
@@ -249,8 +250,103 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 			fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + R[s - 1 + p], (t >> 32) * (uint32_t)kBase);
 		}
 		uint32_t slot;
-		if (checkpoint_slot(fp, pp, k, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
+		if (passes(fp, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
 	}
+}
+
+// The same index built in LDS: one 1024-thread block per pair holds the
+// pair's whole table (cap x u32 <= kBuildLdsMaxBytes), so the first-found
+// minimum is a ds_min_u32 instead of a memory-side atomic (device-scope
+// atomics are not performed in an XCD's L2), and the finished table — empty
+// slots included — is written out once with coalesced stores (no memset).
+constexpr uint32_t kBuildLdsBlock = 1024;
+
+__global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(EncodeArgs a, uint32_t lds_cap) {
+	extern __shared__ uint32_t T[];
+	__shared__ uint64_t ob[256];
+	const uint32_t pair = blockIdx.x;
+	const uint32_t tid = threadIdx.x;
+	const PairPlanDev pp = a.pplan[pair];
+	if (pp.q > lds_cap) return;   // built by correcting_build_kernel
+	const PairDev pd = a.pairs[pair];
+	const uint32_t cap = (uint32_t)pp.q;
+	uint32_t* H = a.ctab + pp.tab_base;
+	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) T[i] = kNone;
+	if (tid < 256) {
+		const uint64_t top = a.powc[0];
+		ob[tid] = fold61c((uint64_t)tid * (uint32_t)top, (uint64_t)tid * (uint32_t)(top >> 32));
+	}
+	__syncthreads();
+	const uint32_t p = a.p;
+	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
+	if (seeds > 0 && pd.v_len > 0) {
+		const uint8_t* R = a.ref + pd.r_off;
+		const uint64_t k = a.kcls[pair];
+		const Ckpt ck = make_ckpt(pp.f_size, pp.f_magic, pp.m, k, pp.q);
+		// the checkpoint path is chosen once per pair (uniform), so the
+		// unrolled seed loop below has no per-seed branches
+		auto run = [&](auto mode) {
+			constexpr int kMode = decltype(mode)::value;   // 0: m = 2^s, 1: FP64, 2: Barrett
+			auto insert = [&](uint64_t fp, uint32_t off) {
+				uint32_t slot;
+				bool pass;
+				if constexpr (kMode == 0) {
+					const uint32_t f = mod_q_small(fp, ck.mf);
+					slot = f >> ck.mshift;
+					pass = (f & ((1u << ck.mshift) - 1u)) == ck.k && slot < ck.cap;
+				} else if constexpr (kMode == 1) {
+					pass = ckpt_test(fp, ck, &slot);
+				} else {
+					pass = checkpoint_slot(fp, pp, k, &slot);
+				}
+				if (pass) __hip_atomic_fetch_min(&T[slot], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+			};
+			for (uint64_t s0 = (uint64_t)tid * kBuildSeedsPerLane; s0 < seeds;
+			     s0 += (uint64_t)kBuildLdsBlock * kBuildSeedsPerLane) {
+				const uint32_t cnt = (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane);
+				if (p == 16 && cnt == kBuildSeedsPerLane) {
+					uint32_t w[12];   // R[s0 .. s0+47), the 48th byte only if it exists
+					__builtin_memcpy(w, R + s0, 32);
+					if (s0 + 48 <= pd.r_len) {
+						__builtin_memcpy(w + 8, R + s0 + 32, 16);
+					} else {
+						__builtin_memcpy(w + 8, R + s0 + 32, 12);
+						w[11] = (uint32_t)R[s0 + 44] | ((uint32_t)R[s0 + 45] << 8) | ((uint32_t)R[s0 + 46] << 16);
+					}
+					auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+					// two independent rolling chains (seeds 0..15 and 16..31)
+					uint64_t fa = fp16_dot(w[0], w[1], w[2], w[3]);
+					uint64_t fb = fp16_dot(w[4], w[5], w[6], w[7]);
+#pragma unroll
+					for (uint32_t j = 0; j < kBuildSeedsPerLane / 2; ++j) {
+						if (j) {   // roll (hash.c:62-98)
+							const uint64_t ta = mod_m61(fa + kMersenne - ob[byte_at(j - 1)]);
+							const uint64_t tb = mod_m61(fb + kMersenne - ob[byte_at(j + 15)]);
+							fa = fold61c((ta & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 15), (ta >> 32) * (uint32_t)kBase);
+							fb = fold61c((tb & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 31), (tb >> 32) * (uint32_t)kBase);
+						}
+						insert(fa, (uint32_t)(s0 + j));
+						insert(fb, (uint32_t)(s0 + 16 + j));
+					}
+				} else {
+					uint64_t fp = window_fp<0>(R + s0, p, a.powc);
+					for (uint32_t j = 0; j < cnt; ++j) {
+						if (j) {
+							const uint64_t s = s0 + j;
+							const uint64_t t = mod_m61(fp + kMersenne - ob[R[s - 1]]);
+							fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + R[s - 1 + p], (t >> 32) * (uint32_t)kBase);
+						}
+						insert(fp, (uint32_t)(s0 + j));
+					}
+				}
+			}
+		};
+		if (ck.mf.ok && ck.mshift >= 0) run(std::integral_constant<int, 0>{});
+		else if (ck.mf.ok) run(std::integral_constant<int, 1>{});
+		else run(std::integral_constant<int, 2>{});
+	}
+	__syncthreads();
+	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) H[i] = T[i];
 }
 
 // ───────────────────────────── scan ───────────────────────────────────────
@@ -308,6 +404,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 
 	if (vl > 0) {
 		const uint64_t k = uni64(a.kcls[pair]);
+		const Ckpt ck = make_ckpt(pp.f_size, pp.f_magic, pp.m, k, pp.q);
 		uint32_t vc = 0, vs = 0;
 		while (st == 0 && vc + p <= vl) {
 			// ── positions vc .. vc+63: fingerprint, checkpoint, lookup, memcmp ──
@@ -315,13 +412,26 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 			bool hit = false;
 			uint32_t off = kNone;
 			if (pos + p <= vl) {
-				const uint64_t fp = window_fp<0>(V + pos, p, a.powc);
+				uint32_t wv[4];
+				uint64_t fp;
+				if (p == 16) {   // dot-product fingerprint of the 16 bytes (dg_devutil.h)
+					ld16u(V + pos, wv);
+					fp = fp16_dot(wv[0], wv[1], wv[2], wv[3]);
+				} else {
+					fp = window_fp<0>(V + pos, p, a.powc);
+				}
 				uint32_t slot;
-				if (checkpoint_slot(fp, pp, k, &slot)) {
+				if (ck.mf.ok ? ckpt_test(fp, ck, &slot) : checkpoint_slot(fp, pp, k, &slot)) {
 					off = H[slot];
 					if (off != kNone) {   // correcting.c:268-285: verify the seed bytes
-						hit = true;
-						for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
+						if (p == 16) {
+							uint32_t wr[4];
+							ld16u(R + off, wr);
+							hit = ((wr[0] ^ wv[0]) | (wr[1] ^ wv[1]) | (wr[2] ^ wv[2]) | (wr[3] ^ wv[3])) == 0u;
+						} else {
+							hit = true;
+							for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
+						}
 					}
 				}
 			}
@@ -391,13 +501,26 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 	}
 }
 
-hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st) {
+// lds_cap: the largest R index (slots) built in one block's LDS, 0 = none;
+// pairs with larger indexes take the memory-atomic build (their tables must
+// have been cleared to ~0 by the caller).  qmin/qmax: index sizes in the batch.
+hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap,
+                             uint64_t qmin) {
 	(void)p;
 	if (a.n_pairs == 0) return hipSuccess;
 	hipLaunchKernelGGL(correcting_class_kernel, dim3((a.n_pairs + 63) / 64), dim3(64), 0, st, a);
-	if (a.max_seeds) {
-		const dim3 grid(a.n_pairs, (a.max_seeds + kBuildSeedsPerBlock - 1) / kBuildSeedsPerBlock);
-		hipLaunchKernelGGL(correcting_build_kernel, grid, dim3(kBuildBlock), 0, st, a);
+	if (lds_cap && qmin <= lds_cap) {
+		const size_t tb = 4ull * (a.qmax < lds_cap ? a.qmax : lds_cap);
+		hipLaunchKernelGGL(correcting_build_lds_kernel, dim3(a.n_pairs), dim3(kBuildLdsBlock), tb, st, a, lds_cap);
+	}
+	if (a.max_seeds && a.qmax > lds_cap) {
+		// 1-D grid, XCD-aware: block b runs on XCD b mod 8, which takes the
+		// pairs == b (mod 8) one after another, all of a pair's chunks in a
+		// row, so each XCD's L2 holds the few R indexes its atomics hit
+		const uint32_t nchunk = (uint32_t)((a.max_seeds + kBuildSeedsPerBlock - 1) / kBuildSeedsPerBlock);
+		const uint64_t blocks = 8ull * ((a.n_pairs + 7) / 8) * nchunk;
+		if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+		hipLaunchKernelGGL(correcting_build_kernel, dim3((uint32_t)blocks), dim3(kBuildBlock), 0, st, a, nchunk, lds_cap);
 	}
 	const size_t lds = sizeof(RingEnt) * ((size_t)(a.buf_cap ? a.buf_cap : 1) + 1);
 	hipLaunchKernelGGL(correcting_scan_kernel, dim3(a.n_pairs), dim3(64), lds, st, a);

@@ -37,21 +37,21 @@ __device__ __forceinline__ uint64_t mod_q(uint64_t x, uint64_t q, uint64_t magic
 	return r;
 }
 
-// x mod q for q < 2^25 in FP64 (full-rate FMA on CDNA; the 64-bit Barrett
-// above needs four quarter-rate 32x32 multiplies).  x = xh 2^32 + xl:
-//   r1 = xh - floor(xh / q) q        (== xh mod q up to one q either way)
-//   y  = r1 (2^32 mod q) + xl        (|y| < 2^52: exact)
-//   r  = y - floor(y / q) q          (in [-q, 2q), exact)
-// and two unsigned minimums bring r into [0, q).  The quotients are off by at
-// most one because |quotient| * 2^-52 < 1.
+// x mod q for q < 2^23 in FP64 (full-rate FMA on CDNA; the 64-bit Barrett
+// above needs four quarter-rate 32x32 multiplies).  x = xh 2^32 + xl with
+// xh < 2^29:
+//   y = xh (2^32 mod q) + xl         (< 2^52 + 2^32: exact in one FMA)
+//   r = y - floor(y / q) q           (in [-q, 2q), exact)
+// and two unsigned minimums bring r into [0, q).  The quotient is off by at
+// most one because y / q * 2^-52 < 1.
 struct ModQ {
 	double qd, inv, k1;   // q, 1/q, 2^32 mod q
-	bool ok;              // q < 2^25: this path applies
+	bool ok;              // q < 2^23: this path applies
 };
 
 __device__ __forceinline__ ModQ make_modq(uint64_t q, uint64_t magic) {
 	ModQ m;
-	m.ok = q < (1ull << 25);
+	m.ok = q < (1ull << 23);
 	m.qd = (double)q;
 	m.inv = 1.0 / m.qd;
 	m.k1 = (double)mod_q(1ull << 32, q, magic);
@@ -59,9 +59,7 @@ __device__ __forceinline__ ModQ make_modq(uint64_t q, uint64_t magic) {
 }
 
 __device__ __forceinline__ uint32_t mod_q_small(uint64_t x, const ModQ& m) {
-	const double xh = (double)(uint32_t)(x >> 32), xl = (double)(uint32_t)x;
-	const double r1 = __fma_rn(-floor(xh * m.inv), m.qd, xh);
-	const double y = __fma_rn(r1, m.k1, xl);
+	const double y = __fma_rn((double)(uint32_t)(x >> 32), m.k1, (double)(uint32_t)x);
 	const uint32_t u = (uint32_t)(int32_t)__fma_rn(-floor(y * m.inv), m.qd, y);
 	const uint32_t q = (uint32_t)m.qd;
 	const uint32_t v = min(u, u + q);
@@ -71,6 +69,50 @@ __device__ __forceinline__ uint32_t mod_q_small(uint64_t x, const ModQ& m) {
 // slot = x mod q by whichever path applies (m.ok is wave-uniform)
 __device__ __forceinline__ uint32_t slot_of(uint64_t x, const ModQ& m, uint64_t q, uint64_t magic) {
 	return m.ok ? mod_q_small(x, m) : (uint32_t)mod_q(x, q, magic);
+}
+
+// p = 16 fingerprints by byte dot products.  fp = sum_k b_k * c_k mod M with
+// c_k = 263^(15-k); splitting every c_k into its 8 bytes gives
+//   fp = sum_j 2^(8j) * D_j,  D_j = sum_k b_k * byte_j(c_k) < 2^20,
+// and each D_j is four v_dot4_u32_u8 over the window's four dwords (zero
+// constant bytes drop out at compile time).  kFpLimb[j][g] packs byte j of
+// c_{4g..4g+3}.
+constexpr uint32_t kFpLimb[8][4] = {
+    {0x90948E99u, 0xCA791EB5u, 0x61A791F7u, 0x01073157u},
+    {0x1E666240u, 0xAE927B7Cu, 0x6526B587u, 0x00010E94u},
+    {0x58871A1Bu, 0xBBD04668u, 0x2B953A50u, 0x00000115u},
+    {0xC9D97A71u, 0x30104632u, 0x1DF75AB2u, 0x00000001u},
+    {0x5F67B04Du, 0x15C57474u, 0x0124FA32u, 0x00000000u},
+    {0xCCF624B1u, 0xA7A654C3u, 0x00012C35u, 0x00000000u},
+    {0x03E64716u, 0xA94AB12Du, 0x00000135u, 0x00000000u},
+    {0x140F1603u, 0x1D191B13u, 0x00000001u, 0x00000000u},
+};
+
+__device__ __forceinline__ uint64_t fp16_dot(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+	const uint32_t w[4] = {w0, w1, w2, w3};
+	uint32_t D[8];
+#pragma unroll
+	for (int j = 0; j < 8; ++j) {
+		uint32_t acc = 0;
+#pragma unroll
+		for (int g = 0; g < 4; ++g)
+			if (kFpLimb[j][g]) acc = __builtin_amdgcn_udot4(w[g], kFpLimb[j][g], acc, false);
+		D[j] = acc;
+	}
+	// Combine in 32-bit pieces: P_i = D_2i + D_2i+1 2^8 < 2^29 and
+	//   fp = P0 + P1 2^16 + P2 2^32 + P3 2^48  (mod M),
+	// with P3 2^48 = (P3 & 0x1FFF) 2^48 + (P3 >> 13) 2^61 == ... + (P3 >> 13).
+	const uint32_t P0 = D[0] + (D[1] << 8), P1 = D[2] + (D[3] << 8);
+	const uint32_t P2 = D[4] + (D[5] << 8), P3 = D[6] + (D[7] << 8);
+	const uint32_t t = P0 + (P3 >> 13);                 // < 2^30
+	const uint32_t lo = t + (P1 << 16);
+	const uint32_t c = lo < t ? 1u : 0u;
+	const uint32_t hi = P2 + ((P3 & 0x1FFFu) << 16) + (P1 >> 16) + c;   // < 2^31
+	// x = hi 2^32 + lo < 2^63: one Mersenne fold and a final subtract
+	const uint32_t lo2 = lo + (hi >> 29);
+	const uint32_t hi2 = (hi & 0x1FFFFFFFu) + (lo2 < lo ? 1u : 0u);
+	uint64_t r = ((uint64_t)hi2 << 32) | lo2;            // <= 2^61 + 2
+	return r >= kMersenne ? r - kMersenne : r;
 }
 
 // Karp-Rabin fingerprint of d[0..p) (src/c/hash.c:28-38) as a dot product
@@ -100,6 +142,60 @@ __device__ __forceinline__ uint64_t window_fp(const uint8_t* d, uint32_t p,
 	// hi * 2^32 == (hi >> 29) * 2^61 + (hi & (2^29-1)) * 2^32 == (hi >> 29) + ...
 	const uint64_t t = lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29);
 	return mod_m61(t);
+}
+
+// The correcting checkpoint test (correcting.c:164-198): f = fp mod |F|
+// passes iff f mod m == k, and its slot is f / m (< cap).  FP64 path for
+// |F| < 2^23: mod_q_small, then one floor-quotient by m fixed up by one.
+struct Ckpt {
+	ModQ mf;            // |F|
+	double md, inv_m;   // m, 1/m
+	uint32_t k, cap;    // class, slots
+	int32_t mshift;     // log2 m when m is a power of two, else -1
+};
+
+__device__ __forceinline__ Ckpt make_ckpt(uint64_t f_size, uint64_t f_magic, uint64_t m, uint64_t k,
+                                          uint64_t cap) {
+	Ckpt c;
+	c.mf = make_modq(f_size, f_magic);
+	c.md = (double)m;
+	c.inv_m = 1.0 / c.md;
+	c.k = (uint32_t)k;
+	c.cap = cap < 0xFFFFFFFFull ? (uint32_t)cap : 0xFFFFFFFFu;
+	c.mshift = (m & (m - 1)) == 0 && m < (1ull << 31) ? (int32_t)__builtin_ctzll(m) : -1;
+	return c;
+}
+
+// c.mf.ok must hold
+__device__ __forceinline__ bool ckpt_test(uint64_t fp, const Ckpt& c, uint32_t* slot) {
+	if (c.mshift >= 0) {   // m = 2^s (the default --table-size gives m = 1)
+		const uint32_t f = mod_q_small(fp, c.mf);
+		const uint32_t i = f >> c.mshift;
+		*slot = i;
+		return (f & ((1u << c.mshift) - 1u)) == c.k && i < c.cap;
+	}
+	const double fd = (double)mod_q_small(fp, c.mf);
+	double id = floor(fd * c.inv_m);
+	double r = __fma_rn(-id, c.md, fd);
+	if (r < 0.0) { r += c.md; id -= 1.0; }
+	if (r >= c.md) { r -= c.md; id += 1.0; }
+	const uint32_t i = (uint32_t)id;
+	*slot = i;
+	return (uint32_t)r == c.k && i < c.cap;
+}
+
+// 16 bytes at any address: the dwords that hold them (the fifth only when
+// the address is unaligned, so nothing past the last byte's dword is read)
+__device__ __forceinline__ void ld16u(const uint8_t* p, uint32_t (&w)[4]) {
+	const uintptr_t a = (uintptr_t)p;
+	const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+	const uint32_t s = (uint32_t)(a & 3);
+	const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+	const uint32_t d4 = s ? q[4] : 0u;
+	w[0] = __builtin_amdgcn_alignbyte(d1, d0, s);
+	w[1] = __builtin_amdgcn_alignbyte(d2, d1, s);
+	w[2] = __builtin_amdgcn_alignbyte(d3, d2, s);
+	w[3] = __builtin_amdgcn_alignbyte(d4, d3, s);
 }
 
 // Wave-parallel forward match extension (src/c/onepass.c:229-234): number of

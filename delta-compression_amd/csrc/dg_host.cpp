@@ -309,6 +309,8 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
+	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
+	uint64_t qmin = ~0ull;
 	uint32_t wave_prio = 0;    // DG_WAVE_PRIO: onepass16 s_setprio level
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches
 	bool ser_block = false;    // DG_SER_BLOCK=1: block-per-pair serialiser (A/B)
@@ -407,6 +409,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		else
 			bound += 57 + d.v_len + 22 * (d.v_len / p);
 		P->qmax = std::max<uint64_t>(P->qmax, x.q);
+		P->qmin = std::min<uint64_t>(P->qmin, x.q);
 	}
 	P->out_bound = bound;
 	P->total_rec = rec;
@@ -506,6 +509,15 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = getenv("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
+	{
+		const char* cb = getenv("DG_CORR_BUILD");
+		int shm = 0;
+		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
+			shm = 0;
+		// one block's LDS less the 2 KiB byte-out table and some slack
+		if (algo == DG_ALGO_CORRECTING && !(cb && strcmp(cb, "global") == 0) && shm > 4096)
+			P->corr_lds_cap = (uint32_t)((shm - 2048 - 256) / 4);
+	}
 	if (!P->serial_crc) {
 		e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
 		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
@@ -648,8 +660,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			a.ctab = P->d_ctab.as<uint32_t>();
 			a.kcls = P->d_kcls.as<uint64_t>();
 			a.max_seeds = (uint32_t)P->max_seeds;
-			HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
-			HIPCHK(ctx, launch_correcting(a, a.p, st));
+			// the LDS build writes every slot of every index; the global
+			// build only fills, so its tables start empty (~0)
+			if (P->qmax > P->corr_lds_cap) HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
+			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin));
 		}
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[3], st));
 		return DG_OK;

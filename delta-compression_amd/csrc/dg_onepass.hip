@@ -143,50 +143,6 @@ __device__ __forceinline__ uint64_t quad_sum64(uint64_t x) {
 	return x + y;
 }
 
-// p = 16 fingerprints by byte dot products.  fp = sum_k b_k * c_k mod M with
-// c_k = 263^(15-k); splitting every c_k into its 8 bytes gives
-//   fp = sum_j 2^(8j) * D_j,  D_j = sum_k b_k * byte_j(c_k) < 2^20,
-// and each D_j is four v_dot4_u32_u8 over the window's four dwords (zero
-// constant bytes drop out at compile time).  kFpLimb[j][g] packs byte j of
-// c_{4g..4g+3}.
-constexpr uint32_t kFpLimb[8][4] = {
-    {0x90948E99u, 0xCA791EB5u, 0x61A791F7u, 0x01073157u},
-    {0x1E666240u, 0xAE927B7Cu, 0x6526B587u, 0x00010E94u},
-    {0x58871A1Bu, 0xBBD04668u, 0x2B953A50u, 0x00000115u},
-    {0xC9D97A71u, 0x30104632u, 0x1DF75AB2u, 0x00000001u},
-    {0x5F67B04Du, 0x15C57474u, 0x0124FA32u, 0x00000000u},
-    {0xCCF624B1u, 0xA7A654C3u, 0x00012C35u, 0x00000000u},
-    {0x03E64716u, 0xA94AB12Du, 0x00000135u, 0x00000000u},
-    {0x140F1603u, 0x1D191B13u, 0x00000001u, 0x00000000u},
-};
-
-__device__ __forceinline__ uint64_t fp16_dot(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-	const uint32_t w[4] = {w0, w1, w2, w3};
-	uint32_t D[8];
-#pragma unroll
-	for (int j = 0; j < 8; ++j) {
-		uint32_t acc = 0;
-#pragma unroll
-		for (int g = 0; g < 4; ++g)
-			if (kFpLimb[j][g]) acc = __builtin_amdgcn_udot4(w[g], kFpLimb[j][g], acc, false);
-		D[j] = acc;
-	}
-	// Combine in 32-bit pieces: P_i = D_2i + D_2i+1 2^8 < 2^29 and
-	//   fp = P0 + P1 2^16 + P2 2^32 + P3 2^48  (mod M),
-	// with P3 2^48 = (P3 & 0x1FFF) 2^48 + (P3 >> 13) 2^61 == ... + (P3 >> 13).
-	const uint32_t P0 = D[0] + (D[1] << 8), P1 = D[2] + (D[3] << 8);
-	const uint32_t P2 = D[4] + (D[5] << 8), P3 = D[6] + (D[7] << 8);
-	const uint32_t t = P0 + (P3 >> 13);                 // < 2^30
-	const uint32_t lo = t + (P1 << 16);
-	const uint32_t c = lo < t ? 1u : 0u;
-	const uint32_t hi = P2 + ((P3 & 0x1FFFu) << 16) + (P1 >> 16) + c;   // < 2^31
-	// x = hi 2^32 + lo < 2^63: one Mersenne fold and a final subtract
-	const uint32_t lo2 = lo + (hi >> 29);
-	const uint32_t hi2 = (hi & 0x1FFFFFFFu) + (lo2 < lo ? 1u : 0u);
-	uint64_t r = ((uint64_t)hi2 << 32) | lo2;            // <= 2^61 + 2
-	return r >= kMersenne ? r - kMersenne : r;
-}
-
 __device__ __forceinline__ uint64_t fold61(uint64_t lo, uint64_t hi) {
 	// lo + hi * 2^32 mod (2^61 - 1), lo < 2^48, hi < 2^45
 	return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
@@ -525,7 +481,7 @@ struct WinSrc {
 			//    wave shifts; the largest matching d is the earliest writer,
 			//    whose fingerprint rides along.
 			uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
-			if (maxT <= kShortT && q < (1ull << 25)) {
+			if (maxT <= kShortT && q < (1ull << 25)) {   // member keys need slot + 1 < 2^25
 				// Keys tag each slot with its member (slot + 1 | j << 25), so
 				// a shifted key can only equal a lane's own key when it comes
 				// from the same member: no per-shift range test, and the

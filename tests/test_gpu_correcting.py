@@ -142,3 +142,17 @@ def test_correcting_c4_device_batch(dg, ctx, orc, torch_cuda):
         assert bytes(refc[ro:ro + rl].numpy()) == R
         assert bytes(verc[vo:vo + vl].numpy()) == V
         assert bytes(outc[offs[i]:offs[i + 1]].numpy()) == orc.encode(CORRECTING, R, V, p=16, q=1), i
+
+
+@pytest.mark.parametrize("build", ["lds", "global"])
+def test_correcting_build_paths(dg, ctx, orc, monkeypatch, build):
+    """Both R-index builds (one block's LDS per pair, or memory-side atomicMin
+    over a (pair, chunk) grid; pairs whose index fits one block's LDS take
+    the first) give the oracle's bytes.  q = 1 keeps the indexes small enough
+    for LDS; DG_CORR_BUILD=global forces the second."""
+    if build == "global":
+        monkeypatch.setenv("DG_CORR_BUILD", "global")
+    cs = [c for c in random_cases(120, seed=4242) if c[3] == 16]
+    got = dg.encode_batch([(R, V) for _, R, V, _, _ in cs], "correcting", p=16, q=1, ctx=ctx)
+    for (name, R, V, _, _), g in zip(cs, got):
+        assert g == orc.encode(CORRECTING, R, V, p=16, q=1), (name, build)
