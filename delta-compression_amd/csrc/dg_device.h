@@ -140,6 +140,7 @@ struct DecodeArgs {
 	uint64_t* out_len;
 	int32_t* status;
 	CrcSpanDev* out_spans;     // nullable: span i's length := version size (for the dst CRC)
+	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
 };
 
 struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off

@@ -957,6 +957,13 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// 2. parse + apply (encoding.c:111-178, apply.c:229-284)
 	if (ev) HIPCHK(ctx, hipEventRecord(ev[2], st));
 	DecodeArgs a{};
+	{
+		static const uint32_t dbg = [] {
+			const char* e = getenv("DG_DEBUG_BITS");
+			return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+		}();
+		a.dbg = dbg;
+	}
 	a.ref = d_ref;
 	a.delta = d_delta;
 	a.descs = P->d_desc.as<dg_decode_desc_dev>();

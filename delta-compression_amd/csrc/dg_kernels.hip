@@ -632,7 +632,8 @@ __device__ __forceinline__ bool overlap(uint64_t a, uint64_t al, uint64_t b, uin
 // So a window of ~300 commands costs ~40 dependent LDS reads instead of ~300
 // serial header decodes.  The commands are then applied 64 at a time.
 #ifdef DG_ONEPASS_PROF   // profiling build only (make prof): per-phase decode cycles
-enum { DP_FILL, DP_LOAD, DP_N1, DP_DBL, DP_WALK, DP_EXP, DP_HDR, DP_COPY, DP_WAIT, DP_WINDOWS, DP_BATCHES, DP_TOTAL, kDecProfN };
+enum { DP_FILL, DP_LOAD, DP_N1, DP_DBL, DP_WALK, DP_EXP, DP_HDR, DP_COPY, DP_WAIT, DP_WINDOWS, DP_BATCHES, DP_TOTAL,
+       DP_ORDERED, DP_C_CMD, DP_C_FLAT, DP_C_BAR, kDecProfN };
 __device__ unsigned long long g_decode_prof[kDecProfN];
 #define DPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define DPROF_ADD(i, t0) (dprof[(i)] += __builtin_amdgcn_s_memtime() - (t0))
@@ -719,20 +720,28 @@ __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b
 	return c;
 }
 
+// unaligned dword / 16-byte accesses (gfx950 global memory allows them)
+typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+
 // Per-wave LDS scratch of the flat copy.
 struct DecScratch {
-	uint32_t* cum;        // [64] byte prefix per non-empty command
+	uint32_t* cum;        // [64] chunk prefix per non-empty command
 	uint32_t* row;        // [128] row start masks (lo dwords, then hi dwords)
 	const uint8_t** sp;   // [64]
 	uint8_t** dp;         // [64]
+	uint32_t* len;        // [64] bytes per non-empty command
 };
 
 // Copy an independent batch (no command overlaps another one's writes, or
-// in-place, reads): byte j of the batch's concatenation goes to lane j % 64
-// in row j / 64; the owning command comes from per-row start masks (owner =
-// starts before the row + popcount(mask bits <= lane) - 1).  Branch-free per
-// row: owners and addresses, then the loads, then the predicated stores.
-// In-place COPYs whose source and destination overlap are memmoved after.
+// in-place, reads) in 16-byte chunks: chunk j of the batch's concatenation
+// (every command cut into 16-byte chunks, its last one partial) goes to lane
+// j % 64 in row j / 64; the owning command comes from per-row start masks
+// (owner = starts before the row + popcount(mask bits <= lane) - 1).  Full
+// chunks are one unaligned 16-byte load and store; a command's partial last
+// chunk is copied by dwords and bytes, never touching the next command's
+// bytes.  In-place COPYs whose source and destination overlap are memmoved
+// after.
 __device__ void dec_flat_batch(const DecCmd& c, bool inplace, uint8_t* O, const uint8_t* R, const uint8_t* D,
                                const DecScratch& x) {
 	const uint32_t lane = lane_id();
@@ -740,19 +749,19 @@ __device__ void dec_flat_batch(const DecCmd& c, bool inplace, uint8_t* O, const 
 	const bool selfov = c.mine && c.kind == 1 && inplace && c.src != c.dst && overlap(c.src, c.len, c.dst, c.len);
 	const bool noop = c.mine && c.kind == 1 && inplace && c.src == c.dst;
 	const uint32_t flen = (c.mine && !selfov && !noop) ? (uint32_t)c.len : 0u;
-	const uint32_t incl = dec_incl_scan(flen);
-	const uint32_t cum = incl - flen;
-	const uint32_t total = rdlane(incl, 63);
-	const bool nz = flen != 0;
+	const uint32_t fch = (flen + 15u) >> 4;
+	const uint32_t incl = dec_incl_scan(fch);
+	const uint32_t cum = incl - fch;
+	const uint32_t total = rdlane(incl, 63);   // chunks
+	const bool nz = fch != 0;
 	const uint32_t ord = dec_incl_scan(nz ? 1u : 0u) - 1u;
 	if (nz) {
 		x.cum[ord] = cum;
 		x.sp[ord] = sp;
 		x.dp[ord] = O + c.dst;
+		x.len[ord] = flen;
 	}
-	typedef __attribute__((address_space(1))) const uint8_t gcu8;
-	typedef __attribute__((address_space(1))) uint8_t gu8;
-	for (uint32_t r0 = 0; 64 * r0 < total; r0 += 64) {   // 64 rows = 4 KiB per round
+	for (uint32_t r0 = 0; 64 * r0 < total; r0 += 64) {   // 64 rows of 64 chunks = 64 KiB per round
 		x.row[lane] = 0;
 		x.row[64 + lane] = 0;
 		__builtin_amdgcn_s_waitcnt(0xc07f);
@@ -768,27 +777,37 @@ __device__ void dec_flat_batch(const DecCmd& c, bool inplace, uint8_t* O, const 
 		const uint32_t pc = (uint32_t)__builtin_popcountll(mrow);
 		const uint32_t rbase = carry + dec_incl_scan(pc) - pc;   // starts before row r0 + lane
 		const uint32_t nrows = min(64u, (total + 63) / 64 - r0);
-		constexpr int kQ = 16;   // rows per pass (VGPR budget: 4 waves per SIMD)
+		constexpr int kQ = 4;   // rows per pass (VGPR budget: 4 waves per SIMD)
 		for (uint32_t q0 = 0; q0 < nrows; q0 += kQ) {
-			gu8* da[kQ];
-			uint8_t v[kQ];
-			bool ok[kQ];
+			uint8_t* da[kQ];
+			const uint8_t* sa[kQ];
+			u32x4_u v[kQ];
+			uint32_t rem[kQ];
 #pragma unroll
 			for (int uu = 0; uu < kQ; ++uu) {
 				const uint32_t u = q0 + uu;
 				const uint32_t j = 64 * (r0 + u) + lane;
-				ok[uu] = u < nrows && j < total;
+				const bool ok = u < nrows && j < total;
 				const uint64_t m = ((uint64_t)rdlane((uint32_t)(mrow >> 32), u) << 32) | rdlane((uint32_t)mrow, u);
 				const uint32_t oo = rdlane(rbase, u) + (uint32_t)__builtin_popcountll(m & mask_le(lane));
-				const uint32_t o = ok[uu] && oo ? oo - 1u : 0u;
-				const uint32_t off = j - x.cum[o];
-				gcu8* sa = ok[uu] ? (gcu8*)(x.sp[o] + off) : (gcu8*)D;   // invalid rows read a harmless byte
-				da[uu] = (gu8*)(x.dp[o] + off);
-				v[uu] = *sa;
+				const uint32_t o = ok && oo ? oo - 1u : 0u;
+				const uint32_t boff = 16u * (j - x.cum[o]);
+				rem[uu] = ok ? x.len[o] - boff : 0u;   // >= 1 for a valid chunk
+				sa[uu] = x.sp[o] + boff;
+				da[uu] = x.dp[o] + boff;
+				v[uu] = rem[uu] >= 16 ? *reinterpret_cast<const u32x4_u*>(sa[uu]) : u32x4_u{0, 0, 0, 0};
 			}
 #pragma unroll
-			for (int uu = 0; uu < kQ; ++uu)
-				if (ok[uu]) *da[uu] = v[uu];
+			for (int uu = 0; uu < kQ; ++uu) {
+				if (rem[uu] >= 16) {
+					*reinterpret_cast<u32x4_u*>(da[uu]) = v[uu];
+				} else if (rem[uu]) {   // the command's last, partial chunk
+					const uint32_t nd = rem[uu] >> 2;
+					for (uint32_t k = 0; k < nd; ++k)
+						*reinterpret_cast<u32_u*>(da[uu] + 4 * k) = *reinterpret_cast<const u32_u*>(sa[uu] + 4 * k);
+					for (uint32_t k = 4 * nd; k < rem[uu]; ++k) da[uu][k] = sa[uu][k];
+				}
+			}
 		}
 	}
 	for (uint64_t m = __ballot(selfov); m; m &= m - 1) {
@@ -848,14 +867,16 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	uint16_t* N2 = NX;
 	uint16_t* N4 = NX + kDecWin;
 	uint16_t* N8 = NX + 2 * kDecWin;
-	static_assert(kDecWaves * (64 * 4 + 128 * 4 + 64 * 8 + 64 * 8) <= 3 * kDecWin * 2, "scratch fits NX");
+	constexpr uint32_t kScratch = 64 * 4 + 128 * 4 + 64 * 8 + 64 * 8 + 64 * 4;
+	static_assert(kDecWaves * kScratch <= 3 * kDecWin * 2, "scratch fits NX");
 	DecScratch xs;
 	{
-		uint8_t* base = reinterpret_cast<uint8_t*>(NX) + wave * (64 * 4 + 128 * 4 + 64 * 8 + 64 * 8);
+		uint8_t* base = reinterpret_cast<uint8_t*>(NX) + wave * kScratch;
 		xs.sp = reinterpret_cast<const uint8_t**>(base);
 		xs.dp = reinterpret_cast<uint8_t**>(base + 64 * 8);
 		xs.cum = reinterpret_cast<uint32_t*>(base + 128 * 8);
 		xs.row = reinterpret_cast<uint32_t*>(base + 128 * 8 + 64 * 4);
+		xs.len = reinterpret_cast<uint32_t*>(base + 128 * 8 + 64 * 4 + 128 * 4);
 	}
 
 #ifdef DG_ONEPASS_PROF
@@ -895,16 +916,17 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		if ((((uintptr_t)O | (uintptr_t)R) & 15) == 0) {   // 16 B per thread, 4 in flight
 			const uint64_t n16 = init / 16;
 			for (uint64_t b = 0; b < n16; b += 4 * kDecBlock) {
-				uint4 x[4];
+				typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+				u32x4 x[4];
 #pragma unroll
 				for (int u = 0; u < 4; ++u) {
 					const uint64_t q = b + kDecBlock * u + tid;
-					if (q < n16) x[u] = reinterpret_cast<const uint4*>(R)[q];
+					x[u] = q < n16 ? reinterpret_cast<const u32x4*>(R)[q] : u32x4{0, 0, 0, 0};
 				}
 #pragma unroll
 				for (int u = 0; u < 4; ++u) {
 					const uint64_t q = b + kDecBlock * u + tid;
-					if (q < n16) reinterpret_cast<uint4*>(O)[q] = x[u];
+					if (q < n16) reinterpret_cast<u32x4*>(O)[q] = x[u];
 				}
 			}
 			const uint64_t z0 = (init + 15) / 16, z1 = bsz / 16;   // whole zero words [z0, z1)
@@ -1066,15 +1088,24 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		}
 		__syncthreads();
 		if (sh[4]) st = 8;
+		const bool free_win = !sh[5];
+		if (!free_win) DPROF_INC(DP_ORDERED);
 		DPROF_ADD(DP_HDR, th0);
 		DPROF_T(tc0);
 		// ── 6. apply ──
-		if (!st) {
-			if (!sh[5]) {
+		if (!st && !(a.dbg & 0x100)) {   // 0x100: skip the apply (A/B measurement only)
+			if (free_win) {
 				for (uint32_t b = wave; b < nb; b += kDecWaves) {
 					DPROF_INC(DP_BATCHES);
+					DPROF_T(tq0);
 					const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
+#ifdef DG_ONEPASS_PROF
+					asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+					DPROF_ADD(DP_C_CMD, tq0);
+					DPROF_T(tq1);
 					dec_flat_batch(c, inplace, O, R, D, xs);
+					DPROF_ADD(DP_C_FLAT, tq1);
 				}
 			} else if (wave == 0) {
 				for (uint32_t b = 0; b < nb; ++b) {
@@ -1084,7 +1115,9 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 				}
 			}
 		}
+		DPROF_T(tq2);
 		__syncthreads();   // the window's stores complete before the next window
+		DPROF_ADD(DP_C_BAR, tq2);
 		DPROF_ADD(DP_COPY, tc0);
 		pos = next_pos;
 	}
