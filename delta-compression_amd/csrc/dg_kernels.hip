@@ -329,24 +329,39 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 
 	uint64_t reg = 0;
 	constexpr int kPf = 4;   // 16-byte loads in flight per lane
+	// The span's first and last byte relative to the lane's chunk, clamped
+	// to a range that keeps every per-block test in 32-bit arithmetic
+	// (outside [-64, 1024 + 64] they only mean "before" / "after").
+	typedef __attribute__((address_space(1))) const uint64_t gcu64;   // global, not flat: loads
+	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
+	auto clamp32 = [](intptr_t v) -> int32_t {
+		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kCrcLaneBytes + 64 ? (intptr_t)kCrcLaneBytes + 64 : v));
+	};
+	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
+	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
+	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
 	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
 		ulonglong2 xs[kPf];
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
-			const uintptr_t addr = cs + w0 + 16 * u;
+			const int32_t o = (int32_t)(w0 + 16 * u);
 			// words wholly before the data are virtual zeros: no-ops on a zero register
-			if ((intptr_t)(addr + 16 - a0) > 0) xs[u] = *reinterpret_cast<const ulonglong2*>(addr);
-			else xs[u] = make_ulonglong2(0, 0);
+			xs[u] = make_ulonglong2(0, 0);
+			if (o + 16 > z0) {
+				gcu64* g = reinterpret_cast<gcu64*>(cs + w0 + 16 * u);
+				xs[u].x = g[0];
+				xs[u].y = g[1];
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
-			const uintptr_t addr = cs + w0 + 16 * u;
+			const int32_t o = (int32_t)(w0 + 16 * u);
 			uint64_t lo = xs[u].x, hi = xs[u].y;
-			const intptr_t f = (intptr_t)start - (intptr_t)addr;   // first data byte index
-			const intptr_t l = (intptr_t)end - (intptr_t)addr;     // one past last
+			const int32_t f = f0 - o;   // first data byte index in this word
+			const int32_t l = l0 - o;   // one past last
 			if (f > -8 || l < 16) {   // only the span's edges need masking
-				const int fc = (int)max(min(f, (intptr_t)24), (intptr_t)-8);
-				const int lc = (int)max(min(l, (intptr_t)24), (intptr_t)-8);
+				const int fc = max(min(f, 24), -8);
+				const int lc = max(min(l, 24), -8);
 				lo &= byte_mask(fc, lc);
 				hi &= byte_mask(fc - 8, lc - 8);
 				// init = ~0: invert the span's first 8 bytes
