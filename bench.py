@@ -306,7 +306,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "delta-encode GiB/s (device-resident batched pairs)",
+            "metric": "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X",
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
