@@ -86,48 +86,62 @@ __device__ __forceinline__ bool checkpoint_slot(uint64_t fp, const PairPlanDev& 
 	return r == k && i < pp.q;
 }
 
-// 4 bytes at an arbitrary address, from the aligned dwords that hold them
-__device__ __forceinline__ uint32_t ld4u(const uint8_t* p) {
-	const uintptr_t a = (uintptr_t)p;
-	const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-	const uint32_t s = (uint32_t)(a & 3);
-	const uint32_t w0 = w[0];
-	const uint32_t w1 = s ? w[1] : 0u;
-	return __builtin_amdgcn_alignbyte(w1, w0, s);
+// Extensions compare 4 KiB per wave step: 4 chunks of 16 bytes per lane,
+// all loads issued before any compare (the byte streams come from HBM/L2,
+// so a step is one load latency rather than four).
+constexpr int kExtChunks = 4;
+
+// first mismatching byte (0..15) of two 16-byte words, 16 if equal; `back`:
+// in back-offset order (the highest address first)
+__device__ __forceinline__ uint32_t first_diff16(const uint32_t (&x)[4], bool back) {
+	uint32_t bad = 16;
+#pragma unroll
+	for (int g = 3; g >= 0; --g) {   // later groups first, so the nearest wins
+		const uint32_t v = back ? x[3 - g] : x[g];
+		if (v) bad = 4u * g + (back ? ((uint32_t)__builtin_clz(v) >> 3) : ((uint32_t)__builtin_ctz(v) >> 3));
+	}
+	return bad;
 }
 
-// number of equal leading bytes of a[0..) and b[0..), at most lim; 1 KiB per
-// wave step (16 bytes per lane)
+// number of equal leading bytes of a[0..) and b[0..), at most lim
 __device__ uint32_t ext_fwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
 	const uint32_t lane = lane_id();
 	uint32_t ml = 0;
 	while (ml < lim) {
-		const uint32_t base = ml + 16 * lane;
-		uint32_t bad = 16;
-		if (base < lim) {
-			const uint32_t n = umin_(16u, lim - base);
+		uint32_t wa[kExtChunks][4], wb[kExtChunks][4];
 #pragma unroll
-			for (int g = 0; g < 4; ++g) {
-				if (bad == 16 && 4u * g < n) {
-					const uint32_t left = n - 4u * g;
-					if (left >= 4) {
-						const uint32_t x = ld4u(a + base + 4 * g) ^ ld4u(b + base + 4 * g);
-						if (x) bad = 4u * g + ((uint32_t)__builtin_ctz(x) >> 3);
-					} else {   // the last bytes before lim: no read past them
-						uint32_t e = left;
-						for (uint32_t t = 0; t < left; ++t)
-							if (e == left && a[base + 4 * g + t] != b[base + 4 * g + t]) e = t;
-						bad = 4u * g + e;   // == n when all equal: a mismatch at lim
-					}
-				}
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint32_t base = ml + 1024u * u + 16 * lane;
+			if (base + 16 <= lim) {
+				ld16u(a + base, wa[u]);
+				ld16u(b + base, wb[u]);
 			}
 		}
-		const uint64_t m = __ballot(bad < 16);
-		if (m) {
-			const uint32_t f = ffs64(m);
-			return umin_(lim, ml + 16 * f + rdlane(bad, f));
+		uint32_t bad[kExtChunks];
+#pragma unroll
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint32_t base = ml + 1024u * u + 16 * lane;
+			bad[u] = 16;
+			if (base + 16 <= lim) {
+				const uint32_t x[4] = {wa[u][0] ^ wb[u][0], wa[u][1] ^ wb[u][1], wa[u][2] ^ wb[u][2], wa[u][3] ^ wb[u][3]};
+				bad[u] = first_diff16(x, false);
+			} else if (base < lim) {   // the last bytes before lim: no read beyond them
+				const uint32_t n = lim - base;
+				uint32_t e = n;
+				for (uint32_t t = 0; t < n; ++t)
+					if (e == n && a[base + t] != b[base + t]) e = t;
+				bad[u] = e;   // == n when all equal: a mismatch at lim
+			}
 		}
-		ml += 1024;
+#pragma unroll
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint64_t m = __ballot(bad[u] < 16);
+			if (m) {
+				const uint32_t f = ffs64(m);
+				return umin_(lim, ml + 1024u * u + 16 * f + rdlane(bad[u], f));
+			}
+		}
+		ml += 1024u * kExtChunks;
 	}
 	return lim;
 }
@@ -138,37 +152,43 @@ __device__ uint32_t ext_bwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
 	const uint32_t lane = lane_id();
 	uint32_t ml = 0;
 	while (ml < lim) {
-		// lane covers back-offsets [ml + 16*lane, +16): bytes a[-(off+1)]
-		const uint32_t base = ml + 16 * lane;
-		uint32_t bad = 16;
-		if (base < lim) {
-			const uint32_t n = umin_(16u, lim - base);
+		// lane covers back-offsets [base, base + 16): bytes a[-(base+16)] .. a[-(base+1)]
+		uint32_t wa[kExtChunks][4], wb[kExtChunks][4];
 #pragma unroll
-			for (int g = 0; g < 4; ++g) {
-				if (bad == 16 && 4u * g < n) {
-					const uint32_t left = n - 4u * g;
-					if (left >= 4) {
-						// the 4 bytes at back-offsets base+4g .. +3; byte 3 is the nearest
-						const uint32_t o = base + 4 * g + 4;
-						const uint32_t x = ld4u(a - o) ^ ld4u(b - o);
-						if (x) bad = 4u * g + ((uint32_t)__builtin_clz(x) >> 3);
-					} else {   // the last bytes before lim: no read beyond them
-						uint32_t e = left;
-						for (uint32_t t = 0; t < left; ++t) {
-							const uint32_t d = base + 4 * g + t + 1;
-							if (e == left && *(a - d) != *(b - d)) e = t;
-						}
-						bad = 4u * g + e;
-					}
-				}
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint32_t base = ml + 1024u * u + 16 * lane;
+			if (base + 16 <= lim) {
+				ld16u(a - base - 16, wa[u]);
+				ld16u(b - base - 16, wb[u]);
 			}
 		}
-		const uint64_t m = __ballot(bad < 16);
-		if (m) {
-			const uint32_t f = ffs64(m);
-			return umin_(lim, ml + 16 * f + rdlane(bad, f));
+		uint32_t bad[kExtChunks];
+#pragma unroll
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint32_t base = ml + 1024u * u + 16 * lane;
+			bad[u] = 16;
+			if (base + 16 <= lim) {
+				const uint32_t x[4] = {wa[u][0] ^ wb[u][0], wa[u][1] ^ wb[u][1], wa[u][2] ^ wb[u][2], wa[u][3] ^ wb[u][3]};
+				bad[u] = first_diff16(x, true);
+			} else if (base < lim) {   // the last bytes before lim: no read beyond them
+				const uint32_t n = lim - base;
+				uint32_t e = n;
+				for (uint32_t t = 0; t < n; ++t) {
+					const uint32_t d = base + t + 1;
+					if (e == n && *(a - d) != *(b - d)) e = t;
+				}
+				bad[u] = e;
+			}
 		}
-		ml += 1024;
+#pragma unroll
+		for (int u = 0; u < kExtChunks; ++u) {
+			const uint64_t m = __ballot(bad[u] < 16);
+			if (m) {
+				const uint32_t f = ffs64(m);
+				return umin_(lim, ml + 1024u * u + 16 * f + rdlane(bad[u], f));
+			}
+		}
+		ml += 1024u * kExtChunks;
 	}
 	return lim;
 }
