@@ -151,7 +151,6 @@ struct SynthCopy {   // V[dst..+len) = R[src..+len)
 };
 
 // launchers (dg_kernels.hip)
-#ifdef __HIP_PLATFORM_AMD__
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
@@ -169,6 +168,5 @@ hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t p
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);
 hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,
                                   const SynthCopy* cmds, uint32_t n_cmds, hipStream_t st);
-#endif
 
 }  // namespace dg
