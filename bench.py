@@ -109,6 +109,7 @@ def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, 
     """C5: the deltas of this rank's pairs are produced on the device first
     (untimed); one step = dg_decode_plan_run over all of them (reference CRC
     on a side stream, decode, output CRC, verify)."""
+    shard = importlib.import_module("delta_compression_amd.shard")
     enc = dg.EncodePlan(ctx, "onepass", layout, q=q)
     d_arena = torch.empty(enc.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
@@ -149,10 +150,7 @@ def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, 
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stages = plan.stage_times()
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(dist, elapsed, world, "cuda")
     v_bytes = sum(vl for _, _, _, vl in layout)
     d_bytes = o[-1]
     dec_ms = stages.get("decode", 0.0)
@@ -209,18 +207,17 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     dg = load_product()
+    shard = importlib.import_module("delta_compression_amd.shard")   # the orchestration the gloo tests run
     ctx = dg.Context(local)
     npg, L, rate, q, seed_base, desc, algo = CONFIGS[args.config]
     if args.pairs:
         npg = args.pairs
     cfg = (npg, L, rate, q, seed_base, desc, algo)
 
-    # rank 0 decides the pair-index ranges and scatters them (RCCL broadcast)
-    ranges = torch.tensor([[r * npg, (r + 1) * npg] for r in range(world)], dtype=torch.int64,
-                          device="cuda")
-    if world > 1:
-        dist.broadcast(ranges, src=0)
-    lo, hi = [int(x) for x in ranges[rank].tolist()]
+    # rank 0 decides the pair-index ranges and scatters them (RCCL broadcast);
+    # equal-size pairs make the byte-balanced ranges equal index ranges
+    ranges = shard.balanced_ranges([1] * (npg * world), world) if rank == 0 else None
+    lo, hi = shard.scatter_ranges(dist, ranges, world, rank, "cuda")
     n = hi - lo
 
     stream = torch.cuda.Stream()
@@ -253,7 +250,6 @@ def main():
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
-    sizes_all = torch.empty(world * n, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
     def step():
@@ -261,8 +257,7 @@ def main():
                  status.data_ptr(), stream.cuda_stream)
         if world > 1:
             with torch.cuda.stream(stream):
-                sizes = offs[1:] - offs[:-1]
-                dist.all_gather_into_tensor(sizes_all, sizes)
+                shard.gather_sizes(dist, offs[1:] - offs[:-1], world)   # the global output index
 
     for _ in range(args.warmup):
         step()
@@ -288,10 +283,7 @@ def main():
     diff_ms = stages.get("diff", 0.0) * args.steps
     crc_ms = stages.get("crc64", 0.0) * args.steps
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(dist, elapsed, world, "cuda")
 
     in_bytes_rank = sum(rl + vl for _, rl, _, vl in layout)
     total_bytes = in_bytes_rank * world * args.steps
