@@ -619,7 +619,11 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
-		HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu));
+		// beside the differencing: 2 blocks per CU per round of differencing
+		// waves (16 per CU), so the CRC neither crowds one round out nor
+		// trails a multi-round batch (C2: 4096 pairs -> 512 blocks)
+		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
+		HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[1], cs));
 		return DG_OK;
 	};
