@@ -1,21 +1,33 @@
 #!/usr/bin/env python3
 """bench.py — batched delta-encode throughput on MI355X.
 
-Metric (BASELINE.json): "delta-encode GiB/s (device-resident batched pairs)".
-One *step* = one pass of the hot path over one batch already resident in HBM:
-CRC-64/XZ of every R and V, onepass differencing, placement and DLT\\x03
-serialisation into one packed output arena (dg_encode_plan_run), plus — at
-N > 1 — the RCCL all-gather of per-pair delta sizes that builds the global
-output index.  value = sum(|R|+|V|) over all ranks and steps / max-over-ranks
-wall time of the timed region, in GiB/s.
+Metric (BASELINE.json): "delta-encode GiB/s (device-resident batched pairs)
+at 1/2/4/8 MI355X".  One *step* = one pass of the hot path over one batch
+already resident in HBM: CRC-64/XZ of every R and V, onepass differencing,
+placement and DLT\\x03 serialisation into one packed output arena
+(dg_encode_plan_run), plus — at N > 1 — the RCCL all-gather of per-pair delta
+sizes and the prefix sum that builds the global output index.  value =
+sum(|R|+|V|) over all ranks and steps / max-over-ranks wall time of the timed
+region, in GiB/s.
 
-Workload (default, N=1 line): BASELINE configs[1] = C2, 4096 independent
-64 KiB pairs per GPU, 1% random byte substitutions, --table-size 1 (q=4099),
-synthetic inputs generated on the device (DESIGN.md "Synthetic inputs").
-Pairs shard across ranks by contiguous index ranges (weak scaling).
+The printed line is the C2 workload (BASELINE configs[1]: 4096 independent
+64 KiB pairs per GPU, 1% byte substitutions, --table-size 1 -> q = 4099).
+Beside it, under "also", the same run measures the other BASELINE configs on
+the same ranks, each with its own roofline and CPU baseline:
+  c3  8192 x 256 KiB pairs per GPU, 10% edits, onepass, q = 16411 (the config
+      BASELINE shards over 8 GPUs: 65536 pairs on 8);
+  c4  4096 transposition pairs of ~256 KiB per GPU, correcting;
+  c5  1024 in-place deltas per GPU (device-encoded C2 deltas converted by
+      dg_make_inplace(localmin), ~1.1 M commands), decode + src/dst CRC verify.
+Inputs are synthetic and generated on the device (DESIGN.md "Synthetic
+inputs").  Pairs shard across ranks by contiguous index ranges (weak scaling).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL over xGMI).
+Launch: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+WORLD_SIZE in the environment, bench.py starts torch.distributed.run with N
+ranks itself (before any GPU call); under torch.distributed.run it runs as
+one rank per GPU (RCCL over xGMI).  --dry-run brings the ranks up over gloo on
+the CPU and runs only the orchestration (no GPU, no encode, value null): the
+launcher test of tests/test_bench_cpu.py.
 """
 from __future__ import annotations
 
@@ -23,6 +35,9 @@ import argparse
 import importlib.util
 import json
 import os
+import platform
+import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -41,12 +56,15 @@ CONFIGS = {
     "c4": (4096, 262144, -50, 1, 0xC4000000,
            "4096 pairs of ~256 KiB per GPU, 8-64 block transpositions (50% moved), correcting, "
            "--table-size 1", "correcting"),
-    # C5: decode + CRC-64/XZ verify of C2-style deltas (1024 streams, ~1.1M commands)
+    # C5: decode + CRC-64/XZ verify of in-place deltas of C2 pairs (1024 streams, ~1.1M commands)
     "c5": (1024, 65536, 0.01, 1, 0xC2000000,
-           "1024 onepass deltas of C2 pairs (~1.1M COPY/ADD commands), decode + src/dst CRC "
-           "verify on device", "decode"),
+           "1024 in-place deltas of C2 pairs per GPU (device onepass encode + dg_make_inplace "
+           "localmin, ~1.1M COPY/ADD commands), decode + src/dst CRC verify on device", "decode"),
 }
-ALGO_ID = {"onepass": 1, "correcting": 2, "decode": 11}
+# oracle/_ref/ref_bench modes: encode onepass / correcting; decode standard / in-place deltas
+REF_MODE = {"onepass": 1, "correcting": 2, "decode": 12}
+# CPU baseline samples (pairs): ~1-3 s per timed repetition of the reference's src/c
+CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096)}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -57,6 +75,13 @@ def load_product():
         submodule_search_locations=[PKG_DIR])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["delta_compression_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_shard():
+    spec = importlib.util.spec_from_file_location("dg_shard", os.path.join(PKG_DIR, "shard.py"))
+    mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
 
@@ -77,39 +102,251 @@ def pmc_traffic(config, kernel):
     return None, None
 
 
-def cpu_baseline(cfg, n_pairs_sample, threads):
-    """The reference's src/c (oracle/_ref/ref_bench, compiled from
-    /root/reference by oracle/Makefile) on the host cores, bounded sample of
-    the same workload.  Falls back to nothing if the build is absent."""
+# ───────────────────────────── CPU baseline ─────────────────────────────────
+
+def cpu_share() -> int:
+    """Host threads this process may use: the affinity set, capped by
+    OMP_NUM_THREADS where the pool sets it (16 per GPU on the GPU boxes)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def _ref_bench(cfg, pairs, threads, reps=5):
     npg, L, rate, q, seed, _, algo = cfg
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    cmd = [exe, str(REF_MODE[algo]), str(pairs), str(L), str(rate), str(seed), str(threads), str(q),
+           str(reps)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, check=True)
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline(name):
+    """The reference's own src/c (oracle/_ref/ref_bench, compiled from
+    /root/reference by oracle/Makefile) on the host, a bounded sample of the
+    same workload: 1 thread and every thread of this process's CPU share,
+    median of 5 timed repetitions each."""
+    cfg = CONFIGS[name]
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     if not os.path.exists(exe):
         return None
-    cmd = [exe, str(ALGO_ID[algo]), str(n_pairs_sample), str(L), str(rate), str(seed), str(threads),
-           str(q), "3"]
+    n1, nall = CPU_SAMPLE[name]
+    threads = cpu_share()
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True)
-        res = json.loads(r.stdout.strip().splitlines()[-1])
+        one = _ref_bench(cfg, n1, 1)
+        many = _ref_bench(cfg, nall, threads)
     except Exception as e:  # noqa: BLE001
         print(f"cpu_baseline failed: {e}", file=sys.stderr)
         return None
+    algo = cfg[6]
+    work = ("delta_decode + delta_apply_delta_inplace + src/dst CRC checks of in-place "
+            "(localmin) onepass deltas; rate = sum |V| / time" if algo == "decode" else
+            f"{algo} chain crc x2 + delta_diff + delta_place_commands + delta_encode; "
+            "rate = sum(|R|+|V|) / time")
     return {
-        "value": round(res["gib_per_s"], 4),
+        "value": round(many["gib_per_s"], 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "reference",
-        "sample": (f"{n_pairs_sample} pairs x ~{L} B of the same workload, src/c "
-                   + ("delta_decode + apply + src/dst CRC checks" if algo == "decode" else
-                      f"{algo} (crc x2 + diff + place + encode)")
-                   + f", {threads} threads, best of 3"),
+        "sample": (f"src/c {work}; {nall} pairs x ~{cfg[1]} B of the same workload on {threads} "
+                   f"threads, median of {many['reps']} (times {many.get('times_s')})"),
+        "single_thread": {"value": round(one["gib_per_s"], 4), "pairs": n1,
+                          "median_s": one.get("median_s"), "times_s": one.get("times_s")},
+        "nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
     }
 
 
-def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, ver, stream, cfg):
-    """C5: the deltas of this rank's pairs are produced on the device first
-    (untimed); one step = dg_decode_plan_run over all of them (reference CRC
-    on a side stream, decode, output CRC, verify)."""
-    shard = importlib.import_module("delta_compression_amd.shard")
+# ───────────────────────────── device workloads ─────────────────────────────
+
+class Rank:
+    def __init__(self, world, rank, local, dist, torch):
+        self.world, self.rank, self.local, self.dist, self.torch = world, rank, local, dist, torch
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+
+def make_inputs(dg, ctx, torch, cfg, lo, n, stream):
+    npg, L, rate, q, seed_base, desc, algo = cfg
+    if rate >= 0:   # substitution pairs (C2/C3/C5)
+        n_edits = int(rate * L + 0.5)
+        ref = torch.empty(max(n, 1) * L, dtype=torch.uint8, device="cuda")
+        ver = torch.empty(max(n, 1) * L, dtype=torch.uint8, device="cuda")
+        ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L,
+                                                    seed_base + lo, n_edits, stream.cuda_stream),
+                  "synth")
+        return ref, ver, [(i * L, L, i * L, L) for i in range(n)]
+    import ctypes as C   # transposition pairs (C4)
+    pairs = (dg._lib.Pair * max(n, 1))()
+    rb, vb = C.c_uint64(), C.c_uint64()
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate), pairs,
+                                                     C.byref(rb), C.byref(vb), None, None, None), "layout")
+    ref = torch.empty(max(rb.value, 1), dtype=torch.uint8, device="cuda")
+    ver = torch.empty(max(vb.value, 1), dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate), pairs,
+                                                     C.byref(rb), C.byref(vb), ref.data_ptr(),
+                                                     ver.data_ptr(), stream.cuda_stream), "synth")
+    return ref, ver, [(x.r_off, x.r_len, x.v_off, x.v_len) for x in pairs[:n]]
+
+
+def timed(R, args, step):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize;
+    returns the max-over-ranks wall time of the K steps."""
+    torch = R.torch
+    R.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    R.barrier()
+    return time.perf_counter() - t0
+
+
+def bench_encode(name, args, R, dg, ctx, shard, stream):
+    torch = R.torch
+    cfg = CONFIGS[name]
+    npg, L, rate, q, seed_base, desc, algo = cfg
+    if args.pairs:
+        npg = args.pairs
+    total = npg * R.world
+    ranges = shard.balanced_ranges([1] * total, R.world) if R.rank == 0 else None
+    allr = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")
+    lo, hi = allr[R.rank]
+    n = hi - lo
+    ref, ver, layout = make_inputs(dg, ctx, torch, cfg, lo, n, stream)
+    plan = dg.EncodePlan(ctx, algo, layout, q=q)
+    aligned16 = all((r_off | v_off) % 16 == 0 for r_off, _, v_off, _ in layout)
+    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    sizes = torch.empty(n, dtype=torch.int64, device="cuda")
+    gather = shard.SizeGather([b - a for a, b in allr], "cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), offs.data_ptr(),
+                 status.data_ptr(), stream.cuda_stream)
+        if R.world > 1:   # the global output index: all-gather of sizes + prefix sum
+            with torch.cuda.stream(stream):
+                torch.sub(offs[1:], offs[:-1], out=sizes)
+                gather.global_offsets(gather(R.dist, sizes))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    bad = int((status != 0).sum().item())
+    if bad:
+        raise SystemExit(f"{name}: encode failed on {bad} pairs: status {status.unique().tolist()}")
+    if R.world > 1:   # the global index covers every rank's packed deltas
+        tot = offs[-1:].clone()
+        R.dist.all_reduce(tot)
+        if int(gather.offsets[-1].item()) != int(tot.item()):
+            raise SystemExit(f"{name}: global output index inconsistent")
+
+    plan.set_timing(args.steps)   # one HIP-event set per timed step, read after the region
+    elapsed = timed(R, args, step)
+    stages = plan.stage_times()
+    plan.set_timing(0)
+    elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
+
+    in_bytes_rank = sum(rl + vl for _, rl, _, vl in layout)
+    value = in_bytes_rank * R.world * args.steps / elapsed / 2**30
+    diff_ms = stages.get("diff", 0.0)
+    achieved = in_bytes_rank / (diff_ms / 1e3) / 1e9 if diff_ms > 0 else 0.0
+    delta_bytes = int(offs[-1].item())
+    kname = ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
+             else "onepass16_kernel" if aligned16 else "onepass_kernel")
+    traffic, traffic_src = pmc_traffic(name, kname) if npg == CONFIGS[name][0] else (None, None)
+    line = {
+        "metric": "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": R.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": ("synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)"
+                 if rate >= 0 else
+                 "synthetic (splitmix64 R, gen_transpositions.py-style block permutation, "
+                 "generated on device)"),
+        "config": {
+            "workload": desc,
+            "name": name,
+            "algorithm": algo,
+            "pairs_per_gpu": n,
+            "pairs_total": total,
+            "pair_bytes": L,
+            "edit_rate": rate if rate >= 0 else None,
+            "moved_block_pct": -rate if rate < 0 else None,
+            "table_size_floor": q,
+            "q": plan.table_size(0),
+            "seed_len": 16,
+            "delta_bytes_per_gpu": delta_bytes,
+            "parallelism": f"dp{R.world} (pair shards, RCCL index scatter + size all-gather)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kname,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": in_bytes_rank,
+            "algorithmic_bytes_per_pair": "|R| + |V| (both streams read once)",
+            "avg_launch_ms": round(diff_ms, 4),
+            "timing": "HIP events on the run stream around the differencing kernel(s), mean over "
+                      "the timed steps",
+            "crc_ms_per_step": round(stages.get("crc64", 0.0), 4),
+            "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+        },
+        "cpu_baseline": None,
+    }
+    plan.close()
+    del ref, ver, out, offs, status, sizes, gather
+    torch.cuda.empty_cache()
+    return line
+
+
+def bench_decode(name, args, R, dg, ctx, shard, stream):
+    """C5: in-place deltas of this rank's C2-style pairs are produced first
+    (untimed: device onepass encode, then dg_make_inplace(localmin) on the
+    host, as `delta encode --inplace` does); one step = dg_decode_plan_run
+    over all of them (reference CRC on a side stream, decode, output CRC,
+    verify)."""
+    torch = R.torch
+    cfg = CONFIGS[name]
+    npg, L, rate, q, seed_base, desc, algo = cfg
+    if args.pairs:
+        npg = args.pairs
+    total = npg * R.world
+    ranges = shard.balanced_ranges([1] * total, R.world) if R.rank == 0 else None
+    lo, hi = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")[R.rank]
+    n = hi - lo
+    ref, ver, layout = make_inputs(dg, ctx, torch, cfg, lo, n, stream)
     enc = dg.EncodePlan(ctx, "onepass", layout, q=q)
     d_arena = torch.empty(enc.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
@@ -119,15 +356,29 @@ def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, 
     torch.cuda.synchronize()
     assert int(est.abs().sum()) == 0
     o = offs.cpu().tolist()
-    descs = [(r_off, r_len, o[i], o[i + 1] - o[i], v_off, v_len)
+    std = d_arena[:o[-1]].cpu().numpy().tobytes()
+    ref_h = ref.cpu().numpy().tobytes()
+    enc.close()
+    del d_arena, est
+    deltas, commands = [], 0
+    for i, (r_off, r_len, v_off, v_len) in enumerate(layout):
+        d = dg.make_inplace(ref_h[r_off:r_off + r_len], std[o[i]:o[i + 1]], policy="localmin")
+        deltas.append(d)
+        commands += dg.info(d)["num_commands"]
+    del std, ref_h
+    d_offs = [0]
+    for d in deltas:
+        d_offs.append(d_offs[-1] + len(d))
+    d_dev = torch.frombuffer(bytearray(b"".join(deltas)), dtype=torch.uint8).to("cuda")
+    descs = [(r_off, r_len, d_offs[i], len(deltas[i]), i * L, max(r_len, v_len))
              for i, (r_off, r_len, v_off, v_len) in enumerate(layout)]
     plan = dg.DecodePlan(ctx, descs)
-    out = torch.empty_like(ver)
+    out = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     out_len = torch.empty(n, dtype=torch.int64, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
 
     def step():
-        plan.run(ref.data_ptr(), d_arena.data_ptr(), out.data_ptr(), out_len.data_ptr(),
+        plan.run(ref.data_ptr(), d_dev.data_ptr(), out.data_ptr(), out_len.data_ptr(),
                  status.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
@@ -136,52 +387,113 @@ def decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, 
     out.zero_()
     step()
     torch.cuda.synchronize()
-    if (int(status.abs().sum()) != 0 or not torch.equal(out, ver)) and not os.environ.get("DG_DEBUG_BITS"):
-        raise SystemExit(f"decode failed: status {status.unique().tolist()}")   # (DG_DEBUG_BITS: A/B runs only)
+    if int(status.abs().sum()) != 0 or not torch.equal(out, ver[:n * L]):
+        raise SystemExit(f"{name}: decode failed: status {status.unique().tolist()}")
     plan.set_timing(args.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(R, args, step)
     stages = plan.stage_times()
-    elapsed = shard.max_over_ranks(dist, elapsed, world, "cuda")
+    elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
     v_bytes = sum(vl for _, _, _, vl in layout)
-    d_bytes = o[-1]
+    d_bytes = d_offs[-1]
     dec_ms = stages.get("decode", 0.0)
-    # decode_kernel algorithmic bytes: the deltas read, COPY sources read and
-    # the outputs written (<= |delta| + 2 sum|V|)
-    alg = d_bytes + 2 * v_bytes
+    # decode_kernel algorithmic bytes: the deltas read, the initial R image
+    # written, COPY sources read and the outputs written (in place: the
+    # output buffer starts as R) -> |delta| + |R| + 2 |V|
+    r_bytes = sum(rl for _, rl, _, _ in layout)
+    alg = d_bytes + r_bytes + 2 * v_bytes
     achieved = alg / (dec_ms / 1e3) / 1e9 if dec_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(name, "decode_kernel") if npg == CONFIGS[name][0] else (None, None)
+    line = {
+        "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
+        "value": round(v_bytes * R.world * args.steps / elapsed / 2**30, 3),
+        "unit": "GiB/s", "n_gpus": R.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (C2 pairs generated on device; deltas from the device encoder, "
+                "converted to in-place by dg_make_inplace localmin)",
+        "config": {"workload": desc, "name": name, "inplace": True, "policy": "localmin",
+                   "streams_per_gpu": n, "commands_per_gpu": commands, "delta_bytes_per_gpu": d_bytes,
+                   "parallelism": f"dp{R.world} (stream shards)"},
+        "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": alg,
+                     "algorithmic_bytes_per_stream": "|delta| + |R| + 2 |V|",
+                     "avg_launch_ms": round(dec_ms, 4),
+                     "stage_ms": {k: round(v, 4) for k, v in stages.items()}},
+        "cpu_baseline": None,
+    }
+    plan.close()
+    del ref, ver, out, d_dev, out_len, status
+    torch.cuda.empty_cache()
+    return line
+
+
+def run_config(name, args, R, dg, ctx, shard, stream):
+    fn = bench_decode if CONFIGS[name][6] == "decode" else bench_encode
+    line = fn(name, args, R, dg, ctx, shard, stream)
+    if R.world == 1 and R.rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(name)
+    return line
+
+
+# ───────────────────────────── launch ───────────────────────────────────────
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """N > 1 without WORLD_SIZE: run this script under torch.distributed.run
+    (one rank per GPU) as a child process; nothing here touches the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def refuse_ab_switches():
+    """The product library reads no environment; the A/B builds do
+    (make -C delta-compression_amd ab).  A measurement line is never printed
+    with any of those switches, or a variant library, selected."""
+    bad = sorted(k for k in os.environ if k.startswith("DG_"))
+    if bad:
+        raise SystemExit(f"bench.py: refusing to measure with A/B switches set: {bad} "
+                         "(scripts/ab_bench.py runs A/B comparisons)")
+
+
+def dry_run(args, world, rank):
+    """Launcher check on the CPU (gloo): ranks come up, the orchestration of
+    the timed step runs on synthetic sizes; no GPU is touched, value is null."""
+    import torch
+    import torch.distributed as dist
+    shard = load_shard()
+    if world > 1:
+        dist.init_process_group("gloo")
+    npg = CONFIGS[args.config][0]
+    total = npg * world + (world - 1)   # deliberately unequal ranges
+    ranges = shard.balanced_ranges([1] * total, world) if rank == 0 else None
+    allr = shard.all_ranges(dist, ranges, world, rank, "cpu")
+    lo, hi = allr[rank]
+    gather = shard.SizeGather([b - a for a, b in allr], "cpu")
+    sizes = torch.arange(lo, hi, dtype=torch.int64) + 26
+    t0 = time.perf_counter()
+    off = gather.global_offsets(gather(dist, sizes))
+    elapsed = shard.max_over_ranks(dist, time.perf_counter() - t0, world, "cpu")
+    ok = int(off[-1]) == sum(range(total)) + 26 * total
     if rank == 0:
-        line = {
-            "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
-            "value": round(v_bytes * world * args.steps / elapsed / 2**30, 3),
-            "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (C2 pairs generated on device, deltas from the device encoder)",
-            "config": {"workload": cfg[5], "streams_per_gpu": n, "delta_bytes_per_gpu": d_bytes,
-                       "parallelism": f"dp{world} (stream shards)"},
-            "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dec_ms, 4),
-                         "stage_ms": {k: round(v, 4) for k, v in stages.items()}},
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_pairs or 4096, threads)
-        print(json.dumps(line), flush=True)
+        print(json.dumps({"metric": "launcher dry run (no GPU, no encode)", "value": None,
+                          "n_gpus": world, "steps": 0, "warmup": 0, "ranges": allr,
+                          "index_ok": ok, "elapsed_s": elapsed}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 def main():
@@ -190,165 +502,46 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--also", default="c3,c4,c5",
+                    help="extra configs measured in the same run, reported under 'also' "
+                         "('none' to skip)")
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-pairs", type=int, default=0,
-                    help="CPU baseline sample size (default: ~10-30 s of src/c work)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher/orchestration check on the CPU over gloo (no GPU)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        sys.exit(dry_run(args, world, rank))
+    refuse_ab_switches()
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+    R = Rank(world, rank, local, dist, torch)
     dg = load_product()
-    shard = importlib.import_module("delta_compression_amd.shard")   # the orchestration the gloo tests run
+    shard = load_shard()
     ctx = dg.Context(local)
-    npg, L, rate, q, seed_base, desc, algo = CONFIGS[args.config]
-    if args.pairs:
-        npg = args.pairs
-    cfg = (npg, L, rate, q, seed_base, desc, algo)
-
-    # rank 0 decides the pair-index ranges and scatters them (RCCL broadcast);
-    # equal-size pairs make the byte-balanced ranges equal index ranges
-    ranges = shard.balanced_ranges([1] * (npg * world), world) if rank == 0 else None
-    lo, hi = shard.scatter_ranges(dist, ranges, world, rank, "cuda")
-    n = hi - lo
-
     stream = torch.cuda.Stream()
-    if rate >= 0:   # substitution pairs (C2/C3)
-        n_edits = int(rate * L + 0.5)
-        ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-        ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-        ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L,
-                                                    seed_base + lo, n_edits, stream.cuda_stream),
-                  "synth")
-        layout = [(i * L, L, i * L, L) for i in range(n)]
-    else:           # transposition pairs (C4)
-        import ctypes as C
-        pairs = (dg._lib.Pair * n)()
-        rb, vb = C.c_uint64(), C.c_uint64()
-        ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate),
-                                                         pairs, C.byref(rb), C.byref(vb), None, None,
-                                                         None), "layout")
-        ref = torch.empty(rb.value, dtype=torch.uint8, device="cuda")
-        ver = torch.empty(vb.value, dtype=torch.uint8, device="cuda")
-        ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base + lo, n, L, int(-rate),
-                                                         pairs, C.byref(rb), C.byref(vb), ref.data_ptr(),
-                                                         ver.data_ptr(), stream.cuda_stream), "synth")
-        layout = [(x.r_off, x.r_len, x.v_off, x.v_len) for x in pairs]
-    if algo == "decode":
-        return decode_bench(args, dg, ctx, torch, dist, world, rank, n, L, q, layout, ref, ver, stream,
-                            cfg)
-    plan = dg.EncodePlan(ctx, algo, layout, q=q)
-    plan_aligned16 = all((r_off | v_off) % 16 == 0 for r_off, _, v_off, _ in layout)
-    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
-    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-    status = torch.empty(n, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
 
-    def step():
-        plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), offs.data_ptr(),
-                 status.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            with torch.cuda.stream(stream):
-                shard.gather_sizes(dist, offs[1:] - offs[:-1], world)   # the global output index
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if int(status.abs().sum().item()) != 0:
-        raise SystemExit(f"encode failed: status {status.unique().tolist()}")
-
-    # one HIP-event set per timed step, recorded on the streams the kernels
-    # run on; read back only after the timed region
-    plan.set_timing(args.steps)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stages = plan.stage_times()   # per-stage means over the K timed steps
-    plan.set_timing(0)
-    diff_ms = stages.get("diff", 0.0) * args.steps
-    crc_ms = stages.get("crc64", 0.0) * args.steps
-
-    elapsed = shard.max_over_ranks(dist, elapsed, world, "cuda")
-
-    in_bytes_rank = sum(rl + vl for _, rl, _, vl in layout)
-    total_bytes = in_bytes_rank * world * args.steps
-    value = total_bytes / elapsed / 2**30
-    avg_diff_s = diff_ms / args.steps / 1e3
-    achieved = in_bytes_rank / avg_diff_s / 1e9 if avg_diff_s > 0 else 0.0
-    delta_bytes = int(offs[-1].item())
-    kname = ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
-             else "onepass16_kernel" if plan_aligned16 else "onepass_kernel")
-    traffic, traffic_src = pmc_traffic(args.config, kname) if npg == CONFIGS[args.config][0] \
-        else (None, None)
-
+    line = run_config(args.config, args, R, dg, ctx, shard, stream)
+    extras = [c for c in args.also.split(",") if c and c != "none" and c != args.config]
+    if extras:
+        line["also"] = {}
+        for name in extras:
+            line["also"][name] = run_config(name, args, R, dg, ctx, shard, stream)
     if rank == 0:
-        line = {
-            "metric": "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X",
-            "value": round(value, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": ("synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)"
-                     if rate >= 0 else
-                     "synthetic (splitmix64 R, gen_transpositions.py-style block permutation, "
-                     "generated on device)"),
-            "config": {
-                "workload": desc,
-                "algorithm": algo,
-                "pairs_per_gpu": n,
-                "pair_bytes": L,
-                "edit_rate": rate if rate >= 0 else None,
-                "moved_block_pct": -rate if rate < 0 else None,
-                "table_size_floor": q,
-                "q": plan.table_size(0),
-                "seed_len": 16,
-                "delta_bytes_per_gpu": delta_bytes,
-                "parallelism": f"dp{world} (pair shards, RCCL index scatter + size all-gather)",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": kname,
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": in_bytes_rank,
-                "avg_launch_ms": round(avg_diff_s * 1e3, 4),
-                "crc_ms_per_step": round(crc_ms / args.steps, 4),
-                "stage_ms": {k: round(v, 4) for k, v in stages.items()},
-            },
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
-            # bounded sample: about 10-30 s of src/c work on `threads` cores
-            sample = args.cpu_pairs or {"c2": 2048, "c3": 256, "c4": 1024}[args.config]
-            line["cpu_baseline"] = cpu_baseline(cfg, sample, threads)
         print(json.dumps(line), flush=True)
-
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

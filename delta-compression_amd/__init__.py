@@ -32,6 +32,7 @@ from ._lib import (  # noqa: F401
     EncodePlan,
     DecodePlan,
     LIB_PATH,
+    LIMIT_TABLE_POOL_BYTES,
     crc64_xz,
     decode,
     default_context,
@@ -47,5 +48,5 @@ __all__ = [
     "ALGO_ONEPASS", "ALGO_CORRECTING", "ALGO_GREEDY", "SEED_LEN", "TABLE_SIZE",
     "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan", "DecodePlan",
     "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
-    "make_inplace", "status_string", "LIB_PATH",
+    "make_inplace", "status_string", "LIB_PATH", "LIMIT_TABLE_POOL_BYTES",
 ]

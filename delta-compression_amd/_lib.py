@@ -29,8 +29,9 @@ _ALGOS = {"greedy": ALGO_GREEDY, "onepass": ALGO_ONEPASS, "correcting": ALGO_COR
 STATUS = {
     0: "DG_OK", 1: "DG_ERR_INVALID_ARG", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_TOO_LARGE",
     4: "DG_ERR_NO_DEVICE", 5: "DG_ERR_HIP", 6: "DG_ERR_NOMEM", 7: "DG_ERR_CAPACITY",
-    8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC",
+    8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC", 11: "DG_ERR_TABLE_POOL",
 }
+LIMIT_TABLE_POOL_BYTES = 0
 
 
 class DeltaError(RuntimeError):
@@ -113,6 +114,7 @@ def _load() -> C.CDLL:
         "dg_context_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "dg_context_destroy": (None, [vp]),
         "dg_context_stream": (vp, [vp]),
+        "dg_context_set_limit": (C.c_int, [vp, C.c_int, u64]),
         "dg_status_string": (C.c_char_p, [C.c_int]),
         "dg_last_error": (C.c_char_p, [vp]),
         "dg_encode_plan_create": (C.c_int, [vp, C.c_int, C.POINTER(Pair), u32, C.POINTER(DiffOptions), C.POINTER(vp)]),
@@ -200,6 +202,10 @@ class Context:
     @property
     def stream(self) -> int:
         return lib.dg_context_stream(self.handle) or 0
+
+    def set_limit(self, limit: int, value: int):
+        """dg_context_set_limit (e.g. LIMIT_TABLE_POOL_BYTES; 0 = automatic)."""
+        self.check(lib.dg_context_set_limit(self.handle, int(limit), int(value)), "set_limit")
 
     def check(self, rc: int, what: str = ""):
         if rc:

@@ -87,8 +87,7 @@ struct EncodeArgs {
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
 	uint64_t* kcls;            // per pair: checkpoint class k (correcting.c:131-136), computed once
-	uint32_t wave_prio;        // onepass16: s_setprio level (issue priority over the CRC waves)
-	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
+	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
 };
 
 // COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the
@@ -140,7 +139,7 @@ struct DecodeArgs {
 	uint64_t* out_len;
 	int32_t* status;
 	CrcSpanDev* out_spans;     // nullable: span i's length := version size (for the dst CRC)
-	uint32_t dbg;              // A/B switches for measurements (DG_DEBUG_BITS), 0 in production
+	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
 };
 
 struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off
@@ -149,6 +148,12 @@ struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off
 struct SynthCopy {   // V[dst..+len) = R[src..+len)
 	uint64_t dst, src, len;
 };
+
+// Measurement switches of the A/B builds (make ab / make variant, compiled
+// with -DDG_AB_SWITCHES): getenv(name) there, always NULL in the product
+// library, which therefore reads no environment variable that changes the
+// work it does (dg_host.cpp).
+const char* ab_env(const char* name);
 
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);

@@ -108,6 +108,7 @@ struct dg_context {
 	uint64_t* d_xinv = nullptr;         // 16
 	uint64_t kseg = 0;
 	uint32_t n_cu = 256;                // compute units (grid caps)
+	uint64_t table_pool_bytes = 0;      // DG_LIMIT_TABLE_POOL_BYTES (0 = automatic)
 	std::string err;
 	// scratch reused by the host-buffer entry points
 	void* pin = nullptr;
@@ -165,6 +166,7 @@ const char* dg_status_string(int s) {
 	case DG_ERR_MALFORMED: return "malformed delta";
 	case DG_ERR_SRC_CRC: return "source file does not match delta";
 	case DG_ERR_DST_CRC: return "output integrity check failed";
+	case DG_ERR_TABLE_POOL: return "onepass work-table pool exhausted";
 	default: return "unknown status";
 	}
 }
@@ -240,7 +242,24 @@ void dg_context_destroy(dg_context_t* ctx) {
 
 void* dg_context_stream(dg_context_t* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+int dg_context_set_limit(dg_context_t* ctx, int limit, uint64_t value) {
+	if (!ctx) return DG_ERR_INVALID_ARG;
+	switch (limit) {
+	case DG_LIMIT_TABLE_POOL_BYTES: ctx->table_pool_bytes = value; return DG_OK;
+	default: return set_err(ctx, DG_ERR_INVALID_ARG, "unknown limit %d", limit);
+	}
+}
+
 }  // extern "C"
+
+const char* dg::ab_env(const char* name) {
+#ifdef DG_AB_SWITCHES
+	return getenv(name);
+#else
+	(void)name;
+	return nullptr;
+#endif
+}
 
 // ───────────────────────────── CRC planning ───────────────────────────────
 
@@ -311,8 +330,7 @@ struct dg_encode_plan {
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	uint64_t qmin = ~0ull;
-	uint32_t wave_prio = 0;    // DG_WAVE_PRIO: onepass16 s_setprio level
-	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches
+	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
 	bool ser_block = false;    // DG_SER_BLOCK=1: block-per-pair serialiser (A/B)
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
@@ -444,10 +462,15 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->n_crc_spans = (uint32_t)sd.size();
 	P->n_crc_segs = (uint32_t)seg.size();
 
-	// table-tier pool: 2 x qmax u64 per slot
-	const char* env = getenv("DG_TABLE_POOL_BYTES");
-	const uint64_t pool = env ? strtoull(env, nullptr, 0) : (1ull << 30);
+	// table-tier pool: 2 x qmax u64 per table.  Automatic size: one table per
+	// resident onepass wave (CUs x 4 SIMDs x 5 waves) where that fits in
+	// 4 GiB, at least 1 GiB; never more tables than pairs.
 	const uint64_t per = 16ull * std::max<uint64_t>(P->qmax, 1);
+	uint64_t pool = ctx->table_pool_bytes;
+	if (pool == 0) {
+		const uint64_t resident = 20ull * ctx->n_cu;
+		pool = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(resident * per, 4ull << 30));
+	}
 	P->n_tables = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(n, 1), pool / per));
 
 	int bad = 0;
@@ -473,7 +496,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		// DG_FUSED=1: onepass16 serialises in-kernel behind a decoupled look-back.
 		// Off by default: the look-back couples every wave to the slowest pair
 		// before it, which cost 20-25% at C2/C3 on MI355X (profiles/r01_ab_fused_vs_unfused.txt).
-		const char* fz = getenv("DG_FUSED");
+		const char* fz = ab_env("DG_FUSED");
 		P->fused = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
 		           fz && fz[0] == '1';
 	}
@@ -499,18 +522,16 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		delete P;
 		return set_err(ctx, DG_ERR_HIP, "plan upload failed: %s", hipGetErrorString(e));
 	}
-	const char* sc = getenv("DG_SERIAL_CRC");
+	const char* sc = ab_env("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
-	const char* sb = getenv("DG_SER_BLOCK");
+	const char* sb = ab_env("DG_SER_BLOCK");
 	P->ser_block = sb && sb[0] == '1';
-	const char* wp = getenv("DG_WAVE_PRIO");
-	P->wave_prio = wp ? (uint32_t)atoi(wp) : 0;
-	const char* db = getenv("DG_DEBUG_BITS");
+	const char* db = ab_env("DG_DEBUG_BITS");
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
-	const char* cf = getenv("DG_CRC_FIRST");
+	const char* cf = ab_env("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
 	{
-		const char* cb = getenv("DG_CORR_BUILD");
+		const char* cb = ab_env("DG_CORR_BUILD");
 		int shm = 0;
 		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
 			shm = 0;
@@ -648,7 +669,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_locks = P->d_locks.as<uint32_t>();
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)P->opts.buf_cap;
-		a.wave_prio = P->wave_prio;
 		a.dbg = P->dbg;
 		if (P->algo == DG_ALGO_ONEPASS) {
 			if (P->fused) {
@@ -963,7 +983,7 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	DecodeArgs a{};
 	{
 		static const uint32_t dbg = [] {
-			const char* e = getenv("DG_DEBUG_BITS");
+			const char* e = ab_env("DG_DEBUG_BITS");
 			return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
 		}();
 		a.dbg = dbg;

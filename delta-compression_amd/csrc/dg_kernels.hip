@@ -557,12 +557,12 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 // overlap_cap: grid cap when the CRC runs beside another kernel (0 = none).
 // A grid-stride CRC of 2 blocks per CU leaves the co-running kernel its
 // issue slots instead of queueing 32 CRC waves per CU behind it (C2: step
-// 0.400 -> 0.372 ms).  DG_CRC_BLOCKS overrides (A/B).
+// 0.400 -> 0.372 ms).  DG_CRC_BLOCKS overrides (A/B builds only).
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap) {
 	if (a.n_segs) {
 		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
 		static const uint32_t env_cap = [] {
-			const char* e = getenv("DG_CRC_BLOCKS");
+			const char* e = ab_env("DG_CRC_BLOCKS");
 			return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
 		}();
 		const uint32_t cap = env_cap ? env_cap : overlap_cap;
@@ -1108,7 +1108,11 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		DPROF_ADD(DP_HDR, th0);
 		DPROF_T(tc0);
 		// ── 6. apply ──
-		if (!st && !(a.dbg & 0x100)) {   // 0x100: skip the apply (A/B measurement only)
+#ifdef DG_AB_SWITCHES
+		if (!st && !(a.dbg & 0x100)) {   // 0x100: skip the apply (A/B builds only, never the product)
+#else
+		if (!st) {
+#endif
 			if (free_win) {
 				for (uint32_t b = wave; b < nb; b += kDecWaves) {
 					DPROF_INC(DP_BATCHES);

@@ -165,6 +165,11 @@ __device__ __forceinline__ uint32_t mask_transpose_8x4(uint32_t x) {
 
 // ───────────────────────────── table tier ─────────────────────────────────
 
+// A wave waits at most this long (s_memrealtime runs at 100 MHz) for a pool
+// table before its pair fails with DG_ERR_TABLE_POOL.
+constexpr uint64_t kTableWaitTicks = 20ull * 100000000ull;   // 20 s
+constexpr int32_t kStatusTablePool = 11;                     // DG_ERR_TABLE_POOL
+
 __device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
 	return ((unsigned long long)tag << 32) | (0xFFFFFFFFu - rel);
 }
@@ -844,17 +849,26 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				if (!in_table) {
 					in_table = true;
 					if (tslot < 0) {
+						// Holders never wait (a table is released when its pair
+						// ends), so the wait always drains; the wall-clock bound
+						// only guarantees every wave an exit.  Running into it is
+						// a pool-capacity condition, reported as such.
 						uint32_t got = 0xFFFFFFFFu;
-						if (lane == 0) {   // bounded spin over the pool
+						if (lane == 0) {
 							const uint32_t n = a.n_tables;
-							for (uint32_t it = 0; it < (1u << 26) && got == 0xFFFFFFFFu; ++it) {
+							const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+							for (uint32_t it = 0; got == 0xFFFFFFFFu; ++it) {
 								const uint32_t slx = (pair + it) % n;
-								if (atomicCAS(&a.table_locks[slx], 0u, 1u) == 0u) got = slx;
-								else if ((it % n) == n - 1) __builtin_amdgcn_s_sleep(8);
+								if (atomicCAS(&a.table_locks[slx], 0u, 1u) == 0u) {
+									got = slx;
+								} else if ((it % n) == n - 1) {
+									__builtin_amdgcn_s_sleep(32);
+									if (__builtin_amdgcn_s_memrealtime() - t_start > kTableWaitTicks) break;
+								}
 							}
 						}
 						got = rdlane(got, 0);
-						if (got == 0xFFFFFFFFu) { st = 5; scanning = false; break; }
+						if (got == 0xFFFFFFFFu) { st = kStatusTablePool; scanning = false; break; }
 						tslot = (int32_t)got;
 						HV = a.tables + (uint64_t)got * 2ull * a.qmax;
 						HR = HV + a.qmax;
@@ -946,9 +960,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch list, member table, round bitmaps
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
-	if (a.wave_prio == 1) __builtin_amdgcn_s_setprio(1);
-	else if (a.wave_prio == 2) __builtin_amdgcn_s_setprio(2);
-	else if (a.wave_prio >= 3) __builtin_amdgcn_s_setprio(3);
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	WinSrc src;
@@ -1009,9 +1020,9 @@ __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
 	onepass_pair(src, a, pair, pd, pp, src.p, bm);
 }
 
-// DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B measurements)
+// DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B builds only)
 static bool force_global_src() {
-	const char* e = getenv("DG_ONEPASS_GLOBAL");
+	const char* e = ab_env("DG_ONEPASS_GLOBAL");
 	return e && e[0] == '1';
 }
 

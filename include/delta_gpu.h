@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 1
+#define DG_ABI_VERSION 2
 
 /* Defaults mirror src/c/delta.h:21-35. */
 #define DG_SEED_LEN        16
@@ -68,7 +68,10 @@ typedef enum {
 	DG_ERR_CAPACITY    = 7,   /* output arena too small */
 	DG_ERR_MALFORMED   = 8,   /* not a delta / truncated / bad command */
 	DG_ERR_SRC_CRC     = 9,   /* reference does not match src_crc */
-	DG_ERR_DST_CRC     = 10   /* reconstructed output does not match dst_crc */
+	DG_ERR_DST_CRC     = 10,  /* reconstructed output does not match dst_crc */
+	DG_ERR_TABLE_POOL  = 11   /* onepass: no work table came free within the
+	                             wait bound (more long-epoch pairs in flight than
+	                             tables; raise DG_LIMIT_TABLE_POOL_BYTES) */
 } dg_status_t;
 
 /* Numbering matches delta_algorithm_t (src/c/delta.h:85). */
@@ -125,6 +128,16 @@ const char *dg_status_string(int status);
 const char *dg_last_error(const dg_context_t *ctx);
 int dg_abi_version(void);
 
+/* Resource limits of a context; they apply to plans created afterwards.
+ *   DG_LIMIT_TABLE_POOL_BYTES: device bytes for the onepass work tables that
+ *     epochs longer than 256 steps spill into (one table = 16 B x q, held by
+ *     a pair from its first long epoch to its end).  0 = automatic: enough
+ *     tables for every resident wave, capped at 4 GiB (at least 1 GiB).
+ *     Pairs beyond the table count wait for one; a wait longer than the
+ *     bound ends the pair with DG_ERR_TABLE_POOL. */
+#define DG_LIMIT_TABLE_POOL_BYTES 0
+int dg_context_set_limit(dg_context_t *ctx, int limit, uint64_t value);
+
 /* ── batched, device-resident encode: the hot path ───────────────────────
  *
  * A batch is N independent (reference, version) pairs laid out in two device
@@ -168,7 +181,7 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
  * makes every run record its events into one of `slots` event sets (a ring;
  * 0 disables) and resets the run count; dg_encode_plan_stage_times fills up to
  * `n` stage durations (ms), averaged over the last min(runs, slots) runs, and
- * their names ("crc64", "diff", "scan+join", "serialize", "total").  Returns
+ * their names ("crc64", "diff", "scan", "serialize+join", "total").  Returns
  * the number of stages.  No host synchronisation happens until stage_times. */
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,

@@ -11,7 +11,8 @@
  *   2. ref_bench main(): the CPU baseline timed by bench.py's cpu_baseline
  *      leg — a pthread pool, one pair per task, same synthetic inputs and
  *      table size as the GPU run, CRC table warmed first (delta.h:297-312 is
- *      not thread-safe on first use).
+ *      not thread-safe on first use); the rate is taken from the median of
+ *      the timed repetitions (times sorted in the output).
  *
  * Nothing here is part of the product.
  */
@@ -209,6 +210,7 @@ int main(int argc, char **argv)
 		}
 	}
 	double best = 1e30, sum = 0;
+	double *times = malloc((reps > 0 ? reps : 1) * sizeof(double));
 	unsigned long long out_bytes = 0;
 	for (int rep = 0; rep < reps; rep++) {
 		j.next = 0;
@@ -220,16 +222,25 @@ int main(int argc, char **argv)
 		for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
 		double dt = now() - t0;
 		free(th);
+		times[rep] = dt;
 		if (dt < best) best = dt;
 		sum += dt;
 		out_bytes = j.out_bytes;
 	}
+	/* median of the repetitions */
+	for (int a = 1; a < reps; a++)
+		for (int b = a; b > 0 && times[b - 1] > times[b]; b--) {
+			double t = times[b]; times[b] = times[b - 1]; times[b - 1] = t;
+		}
+	double med = reps % 2 ? times[reps / 2] : 0.5 * (times[reps / 2 - 1] + times[reps / 2]);
 	double in_bytes = total_in;
 	printf("{\"pairs\": %zu, \"pair_len\": %zu, \"threads\": %d, \"reps\": %d, "
-	       "\"best_s\": %.6f, \"mean_s\": %.6f, \"in_bytes\": %.0f, "
-	       "\"out_bytes\": %llu, \"gib_per_s\": %.6f}\n",
-	       j.n_pairs, j.len, threads, reps, best, sum / reps, in_bytes,
-	       out_bytes, in_bytes / best / (1024.0 * 1024.0 * 1024.0));
+	       "\"best_s\": %.6f, \"mean_s\": %.6f, \"median_s\": %.6f, \"times_s\": [",
+	       j.n_pairs, j.len, threads, reps, best, sum / reps, med);
+	for (int r = 0; r < reps; r++) printf("%s%.4f", r ? ", " : "", times[r]);
+	printf("], \"in_bytes\": %.0f, \"out_bytes\": %llu, \"gib_per_s\": %.6f}\n",
+	       in_bytes, out_bytes, in_bytes / med / (1024.0 * 1024.0 * 1024.0));
+	free(times);
 	return 0;
 }
 #endif

@@ -40,7 +40,15 @@ def test_library_exports_every_declared_symbol(dg):
 
 
 def test_abi_version(dg):
-    assert dg.lib.dg_abi_version() == 1
+    assert dg.lib.dg_abi_version() == 2
+
+
+def test_product_library_reads_no_environment(dg):
+    """The A/B measurement switches exist only in the A/B builds (make ab);
+    the product library imports no getenv at all."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", dg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "getenv" not in out
 
 
 def test_options_default_matches_reference(dg):

@@ -33,17 +33,15 @@ def _worker(rank, world, port, q):
     sizes_in = [65536 * 2] * 10 + [262144 * 2] * 6
     ranges = shard.balanced_ranges(sizes_in, world) if rank == 0 else None
     lo, hi = shard.scatter_ranges(dist, ranges, world, rank, "cpu")
-    # pretend delta sizes: 1000 + global index
-    n = hi - lo
+    # pretend delta sizes: 1000 + global index; the ranges are unequal
+    # (byte-balanced), and SizeGather pads them internally
+    counts = [b - a for a, b in shard.all_ranges(dist, ranges, world, rank, "cpu")]
     local = torch.arange(lo, hi, dtype=torch.int64) + 1000
-    # equal-length gather: pad to the max range length
-    nmax = torch.tensor([n])
-    dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
-    pad = torch.full((int(nmax),), -1, dtype=torch.int64)
-    pad[:n] = local
-    allsz = shard.gather_sizes(dist, pad, world)
-    allsz = allsz[allsz >= 0]
-    off = shard.global_offsets(allsz)
+    g = shard.SizeGather(counts, "cpu")
+    allsz = g(dist, local).clone()
+    off = g.global_offsets(allsz).clone()
+    again = shard.gather_sizes(dist, local, world, counts)   # one-shot form
+    assert again.tolist() == allsz.tolist()
     t = shard.max_over_ranks(dist, float(rank + 1), world, "cpu")
     q.put((rank, lo, hi, allsz.tolist(), off.tolist(), t))
     dist.destroy_process_group()
@@ -66,6 +64,7 @@ def test_gloo_world2_orchestration():
     # contiguous, covering, byte-balanced ranges
     (r0, lo0, hi0, s0, o0, t0), (r1, lo1, hi1, s1, o1, t1) = res
     assert lo0 == 0 and hi0 == lo1 and hi1 == 16
+    assert hi0 - lo0 != hi1 - lo1   # unequal ranges, no padding by the caller
     assert s0 == s1 == [1000 + i for i in range(16)]
     assert o0 == o1 and o0[-1] == sum(s0)
     assert t0 == t1 == 2.0

@@ -12,7 +12,7 @@ import os
 
 import pytest
 
-from cases import random_cases, small_cases
+from cases import DEFAULT_Q, random_cases, small_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -145,14 +145,14 @@ def test_correcting_c4_device_batch(dg, ctx, orc, torch_cuda):
 
 
 @pytest.mark.parametrize("build", ["lds", "global"])
-def test_correcting_build_paths(dg, ctx, orc, monkeypatch, build):
+def test_correcting_build_paths(dg, ctx, orc, build):
     """Both R-index builds (one block's LDS per pair, or memory-side atomicMin
-    over a (pair, chunk) grid; pairs whose index fits one block's LDS take
-    the first) give the oracle's bytes.  q = 1 keeps the indexes small enough
-    for LDS; DG_CORR_BUILD=global forces the second."""
-    if build == "global":
-        monkeypatch.setenv("DG_CORR_BUILD", "global")
+    over a (pair, chunk) grid) give the oracle's bytes.  The plan picks the
+    LDS build when every pair's index fits one block's LDS: q = 1 keeps the
+    indexes small enough; the default --table-size (q = 1048573) does not
+    fit and takes the global build."""
+    q = 1 if build == "lds" else DEFAULT_Q
     cs = [c for c in random_cases(120, seed=4242) if c[3] == 16]
-    got = dg.encode_batch([(R, V) for _, R, V, _, _ in cs], "correcting", p=16, q=1, ctx=ctx)
+    got = dg.encode_batch([(R, V) for _, R, V, _, _ in cs], "correcting", p=16, q=q, ctx=ctx)
     for (name, R, V, _, _), g in zip(cs, got):
-        assert g == orc.encode(CORRECTING, R, V, p=16, q=1), (name, build)
+        assert g == orc.encode(CORRECTING, R, V, p=16, q=q), (name, build)

@@ -1,0 +1,166 @@
+"""GPU parity at BASELINE's full sizes.
+
+* C3 per GPU: the whole 8192 x 256 KiB, 10%-edit device batch the bench
+  times — every status checked, sampled pairs bit-exact against the oracle,
+  the reference-minted golden deltas of pairs 0..3, and every pair decoded
+  back to V on the device (src/dst CRCs verified there).
+* C5: 1024 in-place deltas (device onepass encode of C2 pairs, converted by
+  dg_make_inplace(localmin)) — sampled deltas byte-identical to the
+  reference's own `encode --inplace` chain, all of them decoded on the device
+  in one plan and checked against V.
+* Work-table pool contention: more long-epoch pairs than pool tables (a
+  4-table pool at the default --table-size), every pair checked against the
+  oracle.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+from cases import DEFAULT_Q
+
+pytestmark = pytest.mark.gpu
+
+ONEPASS = 1
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _golden(name):
+    cases = json.load(open(os.path.join(HERE, "golden", "golden.json")))["cases"]
+    return {c["name"]: c for c in cases}[name]
+
+
+def _synth(dg, ctx, torch, n, L, n_edits, seed):
+    ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L, seed,
+                                                n_edits, None), "synth")
+    return ref, ver
+
+
+def _encode(dg, ctx, torch, ref, ver, layout, q, algo="onepass"):
+    plan = dg.EncodePlan(ctx, algo, layout, q=q)
+    out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+    off = torch.empty(len(layout) + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(len(layout), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), off.data_ptr(),
+             st.data_ptr(), ctx.stream)
+    torch.cuda.synchronize()
+    plan.close()
+    return out, off, st
+
+
+def test_c3_full_batch(dg, ctx, orc, torch_cuda):
+    torch = torch_cuda
+    n, L, seed, ne = 8192, 262144, 0xC3000000, 26214
+    ref, ver = _synth(dg, ctx, torch, n, L, ne, seed)
+    layout = [(i * L, L, i * L, L) for i in range(n)]
+    out, off, st = _encode(dg, ctx, torch, ref, ver, layout, q=1)
+    assert int((st != 0).sum()) == 0, st.unique().tolist()
+    offs = off.cpu().tolist()
+    assert offs[0] == 0 and all(offs[i] < offs[i + 1] for i in range(n))
+
+    def delta(i):
+        return bytes(out[offs[i]:offs[i + 1]].cpu().numpy())
+
+    # the reference's own bytes for pairs 0..3 (tests/golden, minted from src/c)
+    for i in range(4):
+        g = _golden(f"c3_{i}")
+        assert g["seed"] == seed + i and g["n_edits"] == ne
+        assert hashlib.sha256(delta(i)).hexdigest() == g["delta_sha256"], i
+    # a spread sample against the oracle (inputs regenerated on the host)
+    for i in [5, 1023, 2048, 4095, 4096, 6000, 7777, n - 1]:
+        R, V = orc.synth_pair(seed + i, L, ne)
+        assert bytes(ref[i * L:(i + 1) * L].cpu().numpy()) == R
+        assert delta(i) == orc.encode(ONEPASS, R, V, p=16, q=1), i
+    # every pair decodes back to V on the device, CRCs verified there
+    descs = (dg._lib.DecodeDesc * n)(*[
+        dg._lib.DecodeDesc(i * L, L, offs[i], offs[i + 1] - offs[i], i * L, L) for i in range(n)])
+    del st
+    dec = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.check(dg.lib.dg_decode_batch_device(ctx.handle, ref.data_ptr(), out.data_ptr(), descs, n, 0,
+                                            dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(), None),
+              "decode batch")
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert bool((dlen == L).all())
+    assert bool(torch.equal(dec, ver))
+    del ref, ver, out, dec
+    torch.cuda.empty_cache()
+
+
+def test_c5_inplace_full_batch(dg, ctx, orc, torch_cuda):
+    import oracle as O
+    torch = torch_cuda
+    n, L, seed, ne = 1024, 65536, 0xC2000000, 655
+    ref, ver = _synth(dg, ctx, torch, n, L, ne, seed)
+    layout = [(i * L, L, i * L, L) for i in range(n)]
+    out, off, st = _encode(dg, ctx, torch, ref, ver, layout, q=1)
+    assert int(st.abs().sum()) == 0
+    offs = off.cpu().tolist()
+    std = out[:offs[-1]].cpu().numpy().tobytes()
+    ref_h = ref.cpu().numpy().tobytes()
+    deltas, commands = [], 0
+    for i in range(n):
+        d = dg.make_inplace(ref_h[i * L:(i + 1) * L], std[offs[i]:offs[i + 1]], policy="localmin")
+        assert d[4] == 1
+        deltas.append(d)
+        commands += dg.info(d)["num_commands"]
+    assert commands > 1_000_000              # ~1.1 M commands
+    if O.reference_available():              # the reference's own encode --inplace chain
+        refc = O.Reference()
+        for i in range(0, n, 97):
+            R, V = orc.synth_pair(seed + i, L, ne)
+            assert deltas[i] == refc.encode_inplace(ONEPASS, R, V, p=16, q=1, policy=0), i
+    d_offs = [0]
+    for d in deltas:
+        d_offs.append(d_offs[-1] + len(d))
+    d_dev = torch.frombuffer(bytearray(b"".join(deltas)), dtype=torch.uint8).to("cuda")
+    descs = [(i * L, L, d_offs[i], len(deltas[i]), i * L, L) for i in range(n)]
+    plan = dg.DecodePlan(ctx, descs)
+    dec = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    for _ in range(2):   # the plan is reusable
+        dec.zero_()
+        torch.cuda.synchronize()
+        plan.run(ref.data_ptr(), d_dev.data_ptr(), dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(),
+                 ctx.stream)
+        torch.cuda.synchronize()
+        assert int(dst.abs().sum()) == 0
+        assert bool((dlen == L).all())
+        assert bool(torch.equal(dec, ver))
+    plan.close()
+
+
+def test_table_pool_contention(dg, orc, torch_cuda):
+    """256 pairs whose epochs run far past the register history (phase C)
+    share a pool of 4 work tables at the default --table-size: waves wait for
+    tables, every pair completes with status 0 and the oracle's bytes."""
+    torch = torch_cuda
+    ctx = dg.Context(0)
+    ctx.set_limit(dg.LIMIT_TABLE_POOL_BYTES, 4 * 16 * DEFAULT_Q)
+    with pytest.raises(dg.DeltaError):
+        ctx.set_limit(99, 1)
+    rng = random.Random(77)
+    pairs = []
+    for i in range(256):
+        R = rng.randbytes(65536)
+        if i % 2:
+            V = rng.randbytes(65536)                          # one epoch over the whole pair
+        else:
+            a = rng.randrange(1000, 60000)
+            V = R[:a] + rng.randbytes(rng.choice([600, 3000, 9000])) + R[a:]   # long epoch, then a match
+        pairs.append((R, V))
+    got = dg.encode_batch(pairs, "onepass", p=16, q=DEFAULT_Q, ctx=ctx)
+    for i, ((R, V), d) in enumerate(zip(pairs, got)):
+        assert d == orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q), i
+    ctx.close()
