@@ -163,6 +163,28 @@ __device__ __forceinline__ uint32_t mask_transpose_8x4(uint32_t x) {
 	return x;
 }
 
+// Two-probe Bloom filter of slots over W 32-bit LDS words: the slot's low
+// bits and a multiplicative hash.  With 64-256 slots in 2048-4096 bits a
+// probe of an absent slot passes ~0.3-1.5 % of the time instead of 3-6 % with
+// one probe, so far fewer steps need the exact (ballot) resolution.
+template <uint32_t W>
+__device__ __forceinline__ uint32_t bloom_h2(uint32_t s) {
+	constexpr uint32_t lg = W == 64 ? 11u : (W == 128 ? 12u : 0u);
+	static_assert(lg != 0, "64 or 128 words");
+	return (s * 0x9E3779B1u) >> (32u - lg);
+}
+template <uint32_t W>
+__device__ __forceinline__ void bloom_add(uint32_t* b, uint32_t s) {
+	const uint32_t h1 = s & (32u * W - 1u), h2 = bloom_h2<W>(s);
+	atomicOr(&b[h1 >> 5], 1u << (h1 & 31u));
+	atomicOr(&b[h2 >> 5], 1u << (h2 & 31u));
+}
+template <uint32_t W>
+__device__ __forceinline__ bool bloom_has(const uint32_t* b, uint32_t s) {
+	const uint32_t h1 = s & (32u * W - 1u), h2 = bloom_h2<W>(s);
+	return ((b[h1 >> 5] >> (h1 & 31u)) & (b[h2 >> 5] >> (h2 & 31u)) & 1u) != 0u;
+}
+
 // ───────────────────────────── table tier ─────────────────────────────────
 
 // A wave waits at most this long (s_memrealtime runs at 100 MHz) for a pool
@@ -229,6 +251,25 @@ constexpr uint32_t kLook = DG_LOOK_BYTES;   // diagonal batch: lookahead bytes p
 #endif
 constexpr uint32_t kShortT = DG_SHORT_T;    // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
+constexpr uint32_t kListCap = 128;          // cached mismatch-list entries (u16, LDS)
+#ifndef DG_LIST_REUSE
+#define DG_LIST_REUSE 16
+#endif
+#ifndef DG_LIST_CACHE
+#define DG_LIST_CACHE 0   // A/B: +2.5% at C3, -6% at C2 (code layout), off
+#endif
+constexpr bool kListCache = DG_LIST_CACHE;
+#ifndef DG_LIST_MIN_CACHE
+#define DG_LIST_MIN_CACHE 1
+#endif
+constexpr uint32_t kListMinCache = DG_LIST_MIN_CACHE;   // only lists this long are looked up again
+constexpr uint32_t kListReuse = DG_LIST_REUSE;   // reuse a cached list with at least this many entries left
+#ifndef DG_BLOOM_BASE
+#define DG_BLOOM_BASE 48
+#endif
+// look-back choice per round: DPP shifts cost ~6 VALU per step of the
+// longest member, the Bloom filter a fixed ~kBloomBase plus ~10 per member
+constexpr uint32_t kBloomBase = DG_BLOOM_BASE;
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
 struct WinSrc {
@@ -239,6 +280,13 @@ struct WinSrc {
 	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
 	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
 	const uint64_t* powc;
+	// Mismatch list of the diagonal batch, kept across calls (LDS, u16
+	// offsets from lc_base, ascending; the stream end counts as one): the
+	// next call usually starts on one of its entries, so the 2 KiB mask
+	// scan runs once per list instead of once per call.
+	uint16_t* lc;            // kListCap entries
+	uint32_t lc_base = 0, lc_diag = 0, lc_n = 0;
+	bool lc_end = false;     // the list ends with the stream-end entry
 	PROF_DECL
 #ifdef DG_REFILL_PROF
 	uint64_t refill_cycles = 0;
@@ -373,49 +421,85 @@ struct WinSrc {
 		const uint32_t lim = umin32(vl - v0, rl - r0);
 		if (lim < p + 1) return DiagOut{0, 0, 0, 0, 0};
 		[[maybe_unused]] uint64_t tq = PROF_NOW();
-		ensure2(v0, r0, 64 * kLook + 48, true, true);
-		// 1. mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
-		const uint32_t base = kLook * lane;
-		// The lane's 32 bytes of each stream come in as three ds_read_b128 from
-		// the 16-byte-aligned address below them (2-way bank conflicts; word
-		// reads at a 32-byte lane stride are 8-way).  The offset inside the
-		// 16 bytes is wave-uniform (windows and lane chunks are 16-aligned),
-		// so picking the 8 words is a uniform switch plus alignbytes.
-		static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
-		uint32_t wv[8], wr[8];
-		lane_words32(0, v0 + base, wv);
-		lane_words32(1, r0 + base, wr);
-		// byte j of word g first lands at bit 8j + g (one shift-and-or per
-		// word), then a 5-bit index rotation (four delta swaps) moves it to
-		// bit 4g + j, i.e. offset order
-		uint32_t bits = 0;
-#pragma unroll
-		for (uint32_t g = 0; g < 8; ++g) {
-			const uint32_t x = wv[g] ^ wr[g];
-			const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
-			bits |= (t >> (7 - g)) & (0x01010101u << g);
+		// 1. the list of mismatch offsets: entries i0.. of the cached list when
+		//    (v0, r0) is one of them on the same diagonal and enough remain,
+		//    else a new list from v0
+		uint32_t i0 = 0xFFFFFFFFu;
+		if (kListCache && lc_n >= kListMinCache && v0 - r0 == lc_diag && v0 >= lc_base && v0 - lc_base < 65535u) {
+			const uint32_t rel = v0 - lc_base;
+			for (uint32_t c = 0; c < lc_n; c += 64) {
+				const uint32_t e = c + lane < lc_n ? (uint32_t)lc[c + lane] : 0xFFFFFFFFu;
+				const uint64_t m = __ballot(e == rel);
+				if (m) { i0 = c + ffs64(m); break; }
+				if (!__ballot(e < rel)) break;
+			}
+			if (i0 != 0xFFFFFFFFu && lc_n - i0 < kListReuse && !lc_end) i0 = 0xFFFFFFFFu;
 		}
-		bits = mask_transpose_8x4(bits);
-		if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
-			bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
-			if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
+		uint32_t K, rel0, ak, an;
+		bool gap, fresh = false;
+		uint64_t G;
+		for (;;) {
+			if (i0 == 0xFFFFFFFFu) {
+				ensure2(v0, r0, 64 * kLook + 48, true, true);
+				// mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
+				const uint32_t base = kLook * lane;
+				// The lane's 32 bytes of each stream come in as three ds_read_b128 from
+				// the 16-byte-aligned address below them (2-way bank conflicts; word
+				// reads at a 32-byte lane stride are 8-way).  The offset inside the
+				// 16 bytes is wave-uniform (windows and lane chunks are 16-aligned),
+				// so picking the 8 words is a uniform switch plus alignbytes.
+				static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
+				uint32_t wv[8], wr[8];
+				lane_words32(0, v0 + base, wv);
+				lane_words32(1, r0 + base, wr);
+				// byte j of word g first lands at bit 8j + g (one shift-and-or per
+				// word), then a 5-bit index rotation (four delta swaps) moves it to
+				// bit 4g + j, i.e. offset order
+				uint32_t bits = 0;
+	#pragma unroll
+				for (uint32_t g = 0; g < 8; ++g) {
+					const uint32_t x = wv[g] ^ wr[g];
+					const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
+					bits |= (t >> (7 - g)) & (0x01010101u << g);
+				}
+				bits = mask_transpose_8x4(bits);
+				if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
+					bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
+					if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
+				}
+				// ordered list (exclusive prefix of counts), at most kListCap entries
+				const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+				const uint32_t incl = wave_incl_scan(cnt);
+				uint32_t pos = incl - cnt;
+				const uint32_t total = rdlane(incl, 63);
+				for (uint32_t b = bits; b && pos < kListCap; b &= b - 1, ++pos) lc[pos] = (uint16_t)(base + __builtin_ctz(b));
+				lc_n = umin32(total, kListCap);
+				lc_end = lim <= 64 * kLook && total <= kListCap;
+				lc_base = v0;
+				lc_diag = v0 - r0;
+				i0 = 0;
+				fresh = true;
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+			}
+			K = umin32(lc_n - i0, 64u);
+			if (K < 2) return DiagOut{0, 0, 0, 0, 0};
+			rel0 = v0 - lc_base;
+			{
+				// the window must hold every byte the batch's steps read
+				const uint32_t last = (uint32_t)lc[i0 + K - 1] - rel0;
+				ensure2(v0, r0, last + 16 + 8, true, true);
+			}
+			PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
+			tq = PROF_NOW();
+			ak = lane < K ? (uint32_t)lc[i0 + lane] - rel0 : 0xFFFFFFFFu;
+			an = lane + 1 < K ? (uint32_t)lc[i0 + lane + 1] - rel0 : 0xFFFFFFFFu;
+			gap = lane + 1 < K && an - ak > p;   // a long gap follows a_lane
+			G = __ballot(gap);
+			// a cached tail that closes no member: list afresh from v0 instead
+			if (G == 0 && !fresh && !lc_end) { i0 = 0xFFFFFFFFu; continue; }
+			break;
 		}
-		// 2. ordered list of mismatch offsets (exclusive prefix of counts)
-		const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
-		const uint32_t incl = wave_incl_scan(cnt);
-		uint32_t pos = incl - cnt;
-		const uint32_t total = rdlane(incl, 63);
-		for (uint32_t b = bits; b && pos < 64; b &= b - 1, ++pos) mlist[pos] = base + __builtin_ctz(b);
-		__builtin_amdgcn_s_waitcnt(0xc07f);
-		__builtin_amdgcn_wave_barrier();
-		const uint32_t K = umin32(total, 64u);
-		if (K < 2) return DiagOut{0, 0, 0, 0, 0};
-		PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
-		tq = PROF_NOW();
-		const uint32_t ak = lane < K ? mlist[lane] : 0xFFFFFFFFu;
-		const uint32_t an = lane + 1 < K ? mlist[lane + 1] : 0xFFFFFFFFu;
-		const bool gap = lane + 1 < K && an - ak > p;   // a long gap follows a_lane
-		const uint64_t G = __ballot(gap);
 		// 3. the chain of epochs.  From a_0 the chain visits exactly the
 		//    mismatches that follow a long gap: member r starts right after
 		//    the (r-1)-th long gap and ends (first equal step) at the r-th,
@@ -423,7 +507,7 @@ struct WinSrc {
 		//    order, T + 1 steps each, while they fit in 64 lanes and T < 64.
 		const uint64_t gbelow = G & ((1ull << lane) - 1ull);
 		const uint32_t sidx = gbelow ? 64u - (uint32_t)__builtin_clzll(gbelow) : 0u;
-		const uint32_t astart = mlist[sidx];   // sidx <= lane < K
+		const uint32_t astart = (uint32_t)lc[i0 + sidx] - rel0;   // sidx <= lane < K
 		const uint32_t T = gap ? ak + 1 - astart : 0u;
 		const uint64_t tooLong = __ballot(gap && T > 63);
 		const uint32_t kb = tooLong ? ffs64(tooLong) : 64u;
@@ -486,7 +570,8 @@ struct WinSrc {
 			//    wave shifts; the largest matching d is the earliest writer,
 			//    whose fingerprint rides along.
 			uint32_t s1 = 64, s2 = 64, f1 = 0, f2 = 0;
-			if (maxT <= kShortT && q < (1ull << 25)) {   // member keys need slot + 1 < 2^25
+			const bool use_dpp = maxT <= kShortT && 6u * maxT <= kBloomBase + 10u * nm;
+			if (use_dpp && q < (1ull << 25)) {   // member keys need slot + 1 < 2^25
 				// Keys tag each slot with its member (slot + 1 | j << 25), so
 				// a shifted key can only equal a lane's own key when it comes
 				// from the same member: no per-shift range test, and the
@@ -508,7 +593,7 @@ struct WinSrc {
 				s2 = d2 != 0xFFu ? lane - d2 : 64u;
 				f1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s1 << 2), (int)fVl);
 				f2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s2 << 2), (int)fRl);
-			} else if (maxT <= kShortT) {
+			} else if (use_dpp) {
 				uint32_t xv = sV, xr = sR, xfv = fVl, xfr = fRl;
 				for (uint32_t d = 0; d <= maxT; ++d) {
 					if (d) {
@@ -537,34 +622,37 @@ struct WinSrc {
 				__builtin_amdgcn_s_waitcnt(0xc07f);
 				__builtin_amdgcn_wave_barrier();
 				if (live) {
-					atomicOr(&bmv[(sV >> 5) & 63u], 1u << (sV & 31u));
-					atomicOr(&bmr[(sR >> 5) & 63u], 1u << (sR & 31u));
+					bloom_add<64>(bmv, sV);
+					bloom_add<64>(bmr, sR);
 				}
 				__builtin_amdgcn_s_waitcnt(0xc07f);
 				__builtin_amdgcn_wave_barrier();
-				const bool q1 = live && ((bmv[(sR >> 5) & 63u] >> (sR & 31u)) & 1u);
-				const bool q2 = live && ((bmr[(sV >> 5) & 63u] >> (sV & 31u)) & 1u);
-				const uint64_t Q1 = __ballot(q1), Q2 = __ballot(q2);
-				for (uint64_t w = Q1 | Q2; w; w &= w - 1) {
+				const bool q1 = live && bloom_has<64>(bmv, sR);
+				const uint64_t Q1 = __ballot(q1);
+				for (uint64_t w = Q1; w; w &= w - 1) {
 					const uint32_t L = ffs64(w);
 					const uint64_t range = mask_le(L) & ~((1ull << rdlane(fb, L)) - 1ull);   // [fb_L, L]
-					if ((Q1 >> L) & 1u) {
-						const uint64_t m = __ballot(sV == rdlane(sR, L)) & range;
-						if (m) {
-							const uint32_t c = ffs64(m);
-							const uint32_t fc = rdlane(fVl, c);
-							s1 = lane == L ? c : s1;
-							f1 = lane == L ? fc : f1;
-						}
+					const uint64_t m = __ballot(sV == rdlane(sR, L)) & range;
+					if (m) {
+						const uint32_t c = ffs64(m);
+						const uint32_t fc = rdlane(fVl, c);
+						s1 = lane == L ? c : s1;
+						f1 = lane == L ? fc : f1;
 					}
-					if ((Q2 >> L) & 1u) {
-						const uint64_t m = __ballot(sR == rdlane(sV, L)) & range;
-						if (m) {
-							const uint32_t c = ffs64(m);
-							const uint32_t fc = rdlane(fRl, c);
-							s2 = lane == L ? c : s2;
-							f2 = lane == L ? fc : f2;
-						}
+				}
+				// lookup 2 matters only where lookup 1 neither hit the diagonal
+				// nor found a fingerprint-equal candidate (step 6 below)
+				const bool hit1 = s1 == lane && t == jT, bad1 = s1 != 64 && s1 != lane && f1 == fRl;
+				const bool need2 = live && !hit1 && !bad1 && bloom_has<64>(bmr, sV);
+				for (uint64_t w = __ballot(need2); w; w &= w - 1) {
+					const uint32_t L = ffs64(w);
+					const uint64_t range = mask_le(L) & ~((1ull << rdlane(fb, L)) - 1ull);   // [fb_L, L]
+					const uint64_t m = __ballot(sR == rdlane(sV, L)) & range;
+					if (m) {
+						const uint32_t c = ffs64(m);
+						const uint32_t fc = rdlane(fRl, c);
+						s2 = lane == L ? c : s2;
+						f2 = lane == L ? fc : f2;
 					}
 				}
 			}
@@ -796,12 +884,12 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				}
 				__builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
 				__builtin_amdgcn_wave_barrier();
-				if (cv) atomicOr(&bm[(sV >> 5) & (BW - 1u)], 1u << (sV & 31u));
-				if (cr) atomicOr(&bm[BW + ((sR >> 5) & (BW - 1u))], 1u << (sR & 31u));
+				if (cv) bloom_add<BW>(bm, sV);
+				if (cr) bloom_add<BW>(bm + BW, sR);
 				__builtin_amdgcn_s_waitcnt(0xc07f);
 				__builtin_amdgcn_wave_barrier();
-				const bool p1 = cr && ((bm[(sR >> 5) & (BW - 1u)] >> (sR & 31u)) & 1u);
-				const bool p2 = cv && ((bm[BW + ((sV >> 5) & (BW - 1u))] >> (sV & 31u)) & 1u);
+				const bool p1 = cr && bloom_has<BW>(bm, sR);
+				const bool p2 = cv && bloom_has<BW>(bm + BW, sV);
 				const uint64_t m1 = __ballot(p1), m2 = __ballot(p2);
 				// steps phase A already ruled out are skipped
 				const uint32_t j0 = (Src::kPhaseA && c == 0 && !skipA) ? 8u : 0u;
@@ -957,7 +1045,8 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
-	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch list, member table, round bitmaps
+	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
+	__shared__ uint16_t lcache[kListCap];   // the diagonal batch's mismatch list
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
@@ -969,6 +1058,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	src.len[1] = (uint32_t)pd.r_len;
 	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
 	src.win = (lds_u8*)win;
+	src.lc = lcache;
 	src.powc = a.powc;
 	PROF_INIT(src)
 	[[maybe_unused]] const uint64_t t_start = PROF_NOW_R();
