@@ -273,8 +273,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     achieved = in_bytes_rank / (diff_ms / 1e3) / 1e9 if diff_ms > 0 else 0.0
     delta_bytes = int(offs[-1].item())
     kname = ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
+             else "member_scan_kernel + member_verify_kernel + onepass16_kernel" if plan.members
              else "onepass16_kernel" if aligned16 else "onepass_kernel")
     traffic, traffic_src = pmc_traffic(name, kname) if npg == CONFIGS[name][0] else (None, None)
+    members = plan.members
     line = {
         "metric": "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -303,6 +305,8 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "table_size_floor": q,
             "q": plan.table_size(0),
             "seed_len": 16,
+            "onepass_chain": ("verified diagonal members" if members else "per-pair chain")
+                             if algo == "onepass" else None,
             "delta_bytes_per_gpu": delta_bytes,
             "parallelism": f"dp{R.world} (pair shards, RCCL index scatter + size all-gather)",
         },
@@ -318,8 +322,8 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "algorithmic_bytes_per_launch": in_bytes_rank,
             "algorithmic_bytes_per_pair": "|R| + |V| (both streams read once)",
             "avg_launch_ms": round(diff_ms, 4),
-            "timing": "HIP events on the run stream around the differencing kernel(s), mean over "
-                      "the timed steps",
+            "timing": "HIP events on the run stream around the differencing kernel(s) (all of "
+                      "them, back to back), mean over the timed steps",
             "crc_ms_per_step": round(stages.get("crc64", 0.0), 4),
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
         },

@@ -32,7 +32,11 @@ from ._lib import (  # noqa: F401
     EncodePlan,
     DecodePlan,
     LIB_PATH,
+    LIMIT_ONEPASS_MEMBERS,
     LIMIT_TABLE_POOL_BYTES,
+    MEMBERS_AUTO,
+    MEMBERS_OFF,
+    MEMBERS_ON,
     crc64_xz,
     decode,
     default_context,
@@ -49,4 +53,5 @@ __all__ = [
     "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan", "DecodePlan",
     "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
     "make_inplace", "status_string", "LIB_PATH", "LIMIT_TABLE_POOL_BYTES",
+    "LIMIT_ONEPASS_MEMBERS", "MEMBERS_AUTO", "MEMBERS_ON", "MEMBERS_OFF",
 ]

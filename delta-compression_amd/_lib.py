@@ -32,6 +32,8 @@ STATUS = {
     8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC", 11: "DG_ERR_TABLE_POOL",
 }
 LIMIT_TABLE_POOL_BYTES = 0
+LIMIT_ONEPASS_MEMBERS = 1
+MEMBERS_AUTO, MEMBERS_ON, MEMBERS_OFF = 0, 1, 2
 
 
 class DeltaError(RuntimeError):
@@ -120,6 +122,7 @@ def _load() -> C.CDLL:
         "dg_encode_plan_create": (C.c_int, [vp, C.c_int, C.POINTER(Pair), u32, C.POINTER(DiffOptions), C.POINTER(vp)]),
         "dg_encode_plan_output_bound": (u64, [vp]),
         "dg_encode_plan_num_pairs": (u32, [vp]),
+        "dg_encode_plan_flags": (u32, [vp]),
         "dg_encode_plan_table_size": (u64, [vp, u32]),
         "dg_encode_plan_run": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_encode_plan_set_timing": (C.c_int, [vp, C.c_int]),
@@ -246,6 +249,11 @@ class EncodePlan:
     @property
     def output_bound(self) -> int:
         return lib.dg_encode_plan_output_bound(self.handle)
+
+    @property
+    def members(self) -> bool:
+        """True when onepass runs through verified diagonal members."""
+        return bool(lib.dg_encode_plan_flags(self.handle) & 1)
 
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)

@@ -88,6 +88,28 @@ struct EncodeArgs {
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
 	uint64_t* kcls;            // per pair: checkpoint class k (correcting.c:131-136), computed once
 	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
+	// member mode (onepass16_kernel after the member kernels, dg_members.hip):
+	// verified diagonal members are taken as they are; nullptr = plain chain
+	const uint32_t* mem_s;     // per member slot (rec_base + k): epoch start s_k
+	const uint32_t* n_mem;     // per pair: closed members K (mem_s[K]: the final epoch)
+	const uint32_t* srec;      // per member: (x, COPY length, ADD head, verified)
+};
+
+// Speculative diagonal members of the onepass chain (dg_members.hip).  The
+// member arrays share the record slots' indexing (rec_base + k): a closed
+// member spans >= p bytes, so K + 1 <= |V| / p + 1 = rec_cap.
+constexpr uint32_t kVerifyWaves = 8;   // verification waves per pair (64 members per pass)
+
+struct SpecArgs {
+	const uint8_t* ref;
+	const uint8_t* ver;
+	const PairDev* pairs;
+	const PairPlanDev* pplan;
+	uint32_t n_pairs;
+	uint32_t* mem_s;           // per member slot: epoch start s_k
+	uint32_t* mem_x;           // per member slot: x_k, the step-T window (s_k + T_k)
+	uint32_t* n_mem;           // per pair: closed members K
+	uint32_t* srec;            // per member slot: (x, len, ADD head, verified)
 };
 
 // COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the
@@ -158,6 +180,7 @@ const char* ab_env(const char* name);
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
+hipError_t launch_members(const SpecArgs& a, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs

@@ -109,6 +109,7 @@ struct dg_context {
 	uint64_t kseg = 0;
 	uint32_t n_cu = 256;                // compute units (grid caps)
 	uint64_t table_pool_bytes = 0;      // DG_LIMIT_TABLE_POOL_BYTES (0 = automatic)
+	uint64_t onepass_members = 0;       // DG_LIMIT_ONEPASS_MEMBERS (0 auto, 1 on, 2 off)
 	std::string err;
 	// scratch reused by the host-buffer entry points
 	void* pin = nullptr;
@@ -246,6 +247,10 @@ int dg_context_set_limit(dg_context_t* ctx, int limit, uint64_t value) {
 	if (!ctx) return DG_ERR_INVALID_ARG;
 	switch (limit) {
 	case DG_LIMIT_TABLE_POOL_BYTES: ctx->table_pool_bytes = value; return DG_OK;
+	case DG_LIMIT_ONEPASS_MEMBERS:
+		if (value > 2) return set_err(ctx, DG_ERR_INVALID_ARG, "onepass members mode %llu", (unsigned long long)value);
+		ctx->onepass_members = value;
+		return DG_OK;
 	default: return set_err(ctx, DG_ERR_INVALID_ARG, "unknown limit %d", limit);
 	}
 }
@@ -322,6 +327,10 @@ struct dg_encode_plan {
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
 	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls;
+	// onepass member mode (dg_members.hip): member arrays share the record
+	// slots' indexing; the verification work queue
+	bool members = false;
+	DevBuf d_mem_s, d_mem_x, d_srec, d_nmem;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
@@ -501,6 +510,32 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		           fz && fz[0] == '1';
 	}
 	if (P->fused) bad |= P->d_lookback.alloc(8ull * std::max<uint32_t>(n, 1));
+	{
+		// member mode: p = 16 onepass over 16-byte aligned pairs (the LDS-window
+		// chain), i.e. the batched hot configuration; DG_NO_MEMBERS=1 (A/B
+		// builds) runs the plain chain
+		// automatic choice by mean pair size for now: measured
+		// (profiles/r02_experiments.md) C3 (256 KiB pairs) +56 %, C2 (64 KiB
+		// pairs, where the plain chain's latency-bound waves overlap the CRC)
+		// -22 %
+		uint64_t vsum = 0;
+		for (uint32_t i = 0; i < n; ++i) vsum += pairs[i].v_len;
+		bool want = n && vsum / n >= (128u << 10);
+		if (ctx->onepass_members == 1) want = true;
+		if (ctx->onepass_members == 2) want = false;
+		const char* nm = ab_env("DG_NO_MEMBERS");
+		if (nm && nm[0] == '1') want = false;
+		const char* fm = ab_env("DG_MEMBERS");
+		if (fm && fm[0] == '1') want = true;
+		P->members = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
+		             !P->fused && want;
+	}
+	if (P->members) {
+		bad |= P->d_mem_s.alloc(4ull * std::max<uint64_t>(rec, 1));
+		bad |= P->d_mem_x.alloc(4ull * std::max<uint64_t>(rec, 1));
+		bad |= P->d_srec.alloc(16ull * std::max<uint64_t>(rec, 1));
+		bad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(n, 1));
+	}
 	if (bad) {
 		delete P;
 		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
@@ -554,6 +589,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 
 uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t* P) { return P ? P->out_bound : 0; }
 uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t* P) { return P ? P->n : 0; }
+uint32_t dg_encode_plan_flags(const dg_encode_plan_t* P) { return P && P->members ? DG_PLAN_MEMBERS : 0u; }
 uint64_t dg_encode_plan_table_size(const dg_encode_plan_t* P, uint32_t i) {
 	return (P && i < P->n) ? P->pp[i].q : 0;
 }
@@ -677,6 +713,22 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.offsets = d_offsets;
 				a.lookback = P->d_lookback.as<unsigned long long>();
 				HIPCHK(ctx, hipMemsetAsync(P->d_lookback.p, 0, 8ull * P->n, st));
+			}
+			if (P->members) {
+				SpecArgs m{};
+				m.ref = d_ref;
+				m.ver = d_ver;
+				m.pairs = a.pairs;
+				m.pplan = a.pplan;
+				m.n_pairs = P->n;
+				m.mem_s = P->d_mem_s.as<uint32_t>();
+				m.mem_x = P->d_mem_x.as<uint32_t>();
+				m.n_mem = P->d_nmem.as<uint32_t>();
+				m.srec = P->d_srec.as<uint32_t>();
+				HIPCHK(ctx, launch_members(m, st));
+				a.mem_s = m.mem_s;
+				a.n_mem = m.n_mem;
+				a.srec = m.srec;
 			}
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 		} else {

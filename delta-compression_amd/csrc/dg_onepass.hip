@@ -95,47 +95,6 @@ extern "C" int dg_refill_prof_reset(void) {
 
 // ───────────────────────────── small helpers ──────────────────────────────
 
-__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
-__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
-
-// x + (lane ^ 1) and x + (lane ^ 2) within quads, via DPP (no LDS traffic)
-__device__ __forceinline__ uint32_t dpp_xor1(uint32_t x) {
-	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-}
-__device__ __forceinline__ uint32_t dpp_xor2(uint32_t x) {
-	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
-}
-// lane l receives x of lane l-1 (lane 0: 0) — DPP wave_shr:1, no LDS
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
-	return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
-}
-// same shift, lane 0 receives 0 (bound_ctrl: one instruction, no old value)
-__device__ __forceinline__ uint32_t wave_shr1z(uint32_t x) {
-	return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x138, 0xF, 0xF, true);
-}
-// inclusive prefix sum over the wave: row_shr 1/2/4/8 inside rows of 16, then
-// row_bcast:15 / row_bcast:31 across rows (all DPP, no LDS round trips)
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
-	x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
-	return x;
-}
-
-// inclusive prefix max over the wave (same DPP network as wave_incl_scan)
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
-	x = umax32(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
-	return x;
-}
-
 __device__ __forceinline__ uint64_t quad_sum64(uint64_t x) {
 	uint64_t y = ((uint64_t)dpp_xor1((uint32_t)(x >> 32)) << 32) | dpp_xor1((uint32_t)x);
 	x += y;
@@ -161,28 +120,6 @@ __device__ __forceinline__ uint32_t mask_transpose_8x4(uint32_t x) {
 	x = delta_swap(x, 0x22222222u, 1);
 	x = delta_swap(x, 0x00AA00AAu, 7);
 	return x;
-}
-
-// Two-probe Bloom filter of slots over W 32-bit LDS words: the slot's low
-// bits and a multiplicative hash.  With 64-256 slots in 2048-4096 bits a
-// probe of an absent slot passes ~0.3-1.5 % of the time instead of 3-6 % with
-// one probe, so far fewer steps need the exact (ballot) resolution.
-template <uint32_t W>
-__device__ __forceinline__ uint32_t bloom_h2(uint32_t s) {
-	constexpr uint32_t lg = W == 64 ? 11u : (W == 128 ? 12u : 0u);
-	static_assert(lg != 0, "64 or 128 words");
-	return (s * 0x9E3779B1u) >> (32u - lg);
-}
-template <uint32_t W>
-__device__ __forceinline__ void bloom_add(uint32_t* b, uint32_t s) {
-	const uint32_t h1 = s & (32u * W - 1u), h2 = bloom_h2<W>(s);
-	atomicOr(&b[h1 >> 5], 1u << (h1 & 31u));
-	atomicOr(&b[h2 >> 5], 1u << (h2 & 31u));
-}
-template <uint32_t W>
-__device__ __forceinline__ bool bloom_has(const uint32_t* b, uint32_t s) {
-	const uint32_t h1 = s & (32u * W - 1u), h2 = bloom_h2<W>(s);
-	return ((b[h1 >> 5] >> (h1 & 31u)) & (b[h2 >> 5] >> (h2 & 31u)) & 1u) != 0u;
 }
 
 // ───────────────────────────── table tier ─────────────────────────────────
@@ -760,8 +697,68 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	bool scanning = vl > 0;
 	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
 	bool skipA = false;         // the epoch is known to be long: phase B from step 0
+
+	// ── member mode (dg_members.hip): verified diagonal members are taken as
+	//    they are, 64 records per pass; the epochs below run only from an
+	//    unverified member until the chain lands on a later member start, and
+	//    for the final epoch ──
+	const bool members = Src::kPhaseA && a.srec != nullptr;
+	uint32_t kmem = 0, Kmem = 0, s_cur = 0;
+	const uint32_t* msp = nullptr;
+	const uint32_t* srp = nullptr;
+	auto take_members = [&]() {
+		while (kmem < Kmem) {
+			const uint32_t n_in = umin32(Kmem - kmem, 64u);
+			const uint32_t j = kmem + lane;
+			uint4 r4 = make_uint4(0u, 0u, 0u, 0u);
+			uint32_t sj = 0;
+			if (lane < n_in) {
+				r4 = *(const uint4*)(srp + 4ull * j);
+				sj = msp[j];
+			}
+			const uint64_t full = n_in == 64 ? ~0ull : ((1ull << n_in) - 1ull);
+			const uint64_t bad = ~__ballot(lane < n_in && r4.w != 0u) & full;
+			const uint32_t take = bad ? ffs64(bad) : n_in;   // the verified prefix
+			if (nrec + take > rec_cap) { st = 7; scanning = false; return; }
+			if (lane < take) *(uint4*)(rec + (uint64_t)kRecWordsOnepass * (nrec + lane)) = make_uint4(r4.x, r4.x, r4.y, r4.z);
+			const uint32_t gap = r4.x - sj;   // ADD [s_j, x_j) before the COPY
+			const uint32_t sz = lane < take ? 13u + (gap ? 9u + gap : 0u) : 0u;
+			dsz += rdlane(wave_incl_scan(sz), 63);
+			nrec += take;
+			kmem += take;
+			if (take < n_in) break;   // member kmem is left to the epochs below
+		}
+		s_cur = uni(msp[kmem]);
+		v0 = r0 = s_cur;
+		at_mismatch = kmem > 0;   // member starts past the first are mismatches
+	};
+	if (members && scanning) {
+		Kmem = uni(a.n_mem[pair]);
+		msp = a.mem_s + pp.rec_base;
+		srp = a.srec + 4ull * pp.rec_base;
+		take_members();
+	}
+
 	while (scanning) {
 		skipA = false;
+		if (members && kmem < Kmem && v0 == r0 && v0 > s_cur) {
+			// did the exact chain land on a later member start? (ascending)
+			uint32_t m = kmem + 1;
+			bool found = false;
+			while (m <= Kmem) {
+				const uint32_t j = m + lane;
+				const uint32_t sj = j <= Kmem ? msp[j] : 0xFFFFFFFFu;
+				const uint64_t eq = __ballot(sj == v0);
+				if (eq) { m += ffs64(eq); found = true; break; }
+				if (__ballot(sj > v0)) break;
+				m += 64;
+			}
+			if (found) {
+				kmem = m;
+				take_members();
+				continue;
+			}
+		}
 		// no match is possible once either stream cannot supply a window at
 		// the epoch start (the reference keeps scanning the other, :102-104)
 		if (v0 + p > vl || r0 + p > rl) break;

@@ -136,6 +136,11 @@ int dg_abi_version(void);
  *     Pairs beyond the table count wait for one; a wait longer than the
  *     bound ends the pair with DG_ERR_TABLE_POOL. */
 #define DG_LIMIT_TABLE_POOL_BYTES 0
+/*   DG_LIMIT_ONEPASS_MEMBERS: how onepass plans (seed length 16, 16-byte
+ *     aligned pairs) run the epoch chain.  0 = automatic, 1 = verified
+ *     diagonal members first (the chain walks only unverified members), 2 =
+ *     the plain per-pair chain.  Output bytes are identical in every mode. */
+#define DG_LIMIT_ONEPASS_MEMBERS 1
 int dg_context_set_limit(dg_context_t *ctx, int limit, uint64_t value);
 
 /* ── batched, device-resident encode: the hot path ───────────────────────
@@ -186,6 +191,10 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
                                const char **names, int n);
+/* How the plan runs (bit flags): DG_PLAN_MEMBERS = onepass through verified
+ * diagonal members (DG_LIMIT_ONEPASS_MEMBERS). */
+#define DG_PLAN_MEMBERS 1u
+uint32_t dg_encode_plan_flags(const dg_encode_plan_t *plan);
 /* Per-pair command statistics of the last run (device pointers owned by the
  * plan, valid until the next run): number of COPY commands and delta size. */
 const uint32_t *dg_encode_plan_copy_counts_device(const dg_encode_plan_t *plan);

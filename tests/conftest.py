@@ -68,3 +68,12 @@ def torch_cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch
+
+
+@pytest.fixture(scope="session", params=["members", "chain"])
+def ctx_mode(dg, request):
+    """A context per onepass chain mode (DG_LIMIT_ONEPASS_MEMBERS): verified
+    diagonal members first, or the plain per-pair chain."""
+    c = dg.Context(0)
+    c.set_limit(dg.LIMIT_ONEPASS_MEMBERS, dg.MEMBERS_ON if request.param == "members" else dg.MEMBERS_OFF)
+    return c

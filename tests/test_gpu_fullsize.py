@@ -55,8 +55,9 @@ def _encode(dg, ctx, torch, ref, ver, layout, q, algo="onepass"):
     return out, off, st
 
 
-def test_c3_full_batch(dg, ctx, orc, torch_cuda):
+def test_c3_full_batch(dg, ctx_mode, orc, torch_cuda):
     torch = torch_cuda
+    ctx = ctx_mode
     n, L, seed, ne = 8192, 262144, 0xC3000000, 26214
     ref, ver = _synth(dg, ctx, torch, n, L, ne, seed)
     layout = [(i * L, L, i * L, L) for i in range(n)]
@@ -141,13 +142,15 @@ def test_c5_inplace_full_batch(dg, ctx, orc, torch_cuda):
     plan.close()
 
 
-def test_table_pool_contention(dg, orc, torch_cuda):
+@pytest.mark.parametrize("mode", ["members", "chain"])
+def test_table_pool_contention(dg, orc, torch_cuda, mode):
     """256 pairs whose epochs run far past the register history (phase C)
     share a pool of 4 work tables at the default --table-size: waves wait for
     tables, every pair completes with status 0 and the oracle's bytes."""
     torch = torch_cuda
     ctx = dg.Context(0)
     ctx.set_limit(dg.LIMIT_TABLE_POOL_BYTES, 4 * 16 * DEFAULT_Q)
+    ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, dg.MEMBERS_ON if mode == "members" else dg.MEMBERS_OFF)
     with pytest.raises(dg.DeltaError):
         ctx.set_limit(99, 1)
     rng = random.Random(77)

@@ -56,13 +56,14 @@ def test_crc_batch_alignments(dg, ctx, orc, torch_cuda):
 # ── onepass encode ───────────────────────────────────────────────────────
 
 @pytest.mark.parametrize("case", small_cases(), ids=lambda c: c[0])
-def test_onepass_small_cases(dg, ctx, orc, case):
+def test_onepass_small_cases(dg, ctx_mode, orc, case):
     name, R, V, p, q = case
-    got = dg.encode(R, V, "onepass", p=p, q=q, ctx=ctx)
+    got = dg.encode(R, V, "onepass", p=p, q=q, ctx=ctx_mode)
     assert got == orc.encode(ONEPASS, R, V, p=p, q=q)
 
 
-def test_onepass_random_batch(dg, ctx, orc):
+def test_onepass_random_batch(dg, ctx_mode, orc):
+    ctx = ctx_mode
     cs = random_cases(300, seed=99)
     by_pq = {}
     for name, R, V, p, q in cs:
@@ -90,10 +91,11 @@ def _device_batch(dg, ctx, torch, n, L, rate, seed, algo="onepass", q=1, check=6
     return plan, ref, ver, out, off, st, n_edits
 
 
-def test_onepass_c2_batch_sample(dg, ctx, orc, torch_cuda):
+def test_onepass_c2_batch_sample(dg, ctx_mode, orc, torch_cuda):
     """C2 geometry (64 KiB pairs, 1% edits, --table-size 1): device-generated
     inputs equal the oracle's generator; sampled pairs bit-exact."""
     torch = torch_cuda
+    ctx = ctx_mode
     n, L, seed = 256, 65536, 0xC2000000
     plan, ref, ver, out, off, st, ne = _device_batch(dg, ctx, torch, n, L, 0.01, seed)
     stc = st.cpu()
@@ -156,8 +158,9 @@ def _golden_inputs(orc, case):
     return orc.synth_random(case["r_seed"], 1 << 20), orc.synth_random(case["v_seed"], 1 << 20)
 
 
-def test_golden_onepass_on_device(dg, ctx, orc):
+def test_golden_onepass_on_device(dg, ctx_mode, orc):
     import hashlib
+    ctx = ctx_mode
     groups = {}
     for c in _golden():
         if c["algo"] != ONEPASS:
@@ -173,8 +176,9 @@ def test_golden_onepass_on_device(dg, ctx, orc):
 
 # ── full C2 batch: every pair decodes back to V on the device ─────────────
 
-def test_c2_full_batch_roundtrip(dg, ctx, orc, torch_cuda):
+def test_c2_full_batch_roundtrip(dg, ctx_mode, orc, torch_cuda):
     torch = torch_cuda
+    ctx = ctx_mode
     n, L, seed = 4096, 65536, 0xC2000000
     plan, ref, ver, out, off, st, ne = _device_batch(dg, ctx, torch, n, L, 0.01, seed)
     assert int(st.abs().sum()) == 0
