@@ -37,6 +37,10 @@ struct PairPlanDev {
 	uint64_t f_size, f_magic;  // |F| and floor((2^64-1)/|F|)
 	uint64_t m, m_magic;       // checkpoint modulus and Barrett
 	uint64_t tab_base;         // first entry of this pair's R index (correcting)
+	// onepass member mode (dg_members.hip)
+	uint64_t mem_base;         // first member slot (n_chunks x kMemChunkSlots slots)
+	uint32_t chunk_base;       // first chunk (index into the per-chunk member counts)
+	uint32_t n_chunks;         // chunks of kMemChunk positions covering [0, min(|R|,|V|)]
 };
 
 struct CrcSegDev {        // one wave's CRC segment
@@ -90,26 +94,32 @@ struct EncodeArgs {
 	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
 	// member mode (onepass16_kernel after the member kernels, dg_members.hip):
 	// verified diagonal members are taken as they are; nullptr = plain chain
-	const uint32_t* mem_s;     // per member slot (rec_base + k): epoch start s_k
-	const uint32_t* n_mem;     // per pair: closed members K (mem_s[K]: the final epoch)
-	const uint32_t* srec;      // per member: (x, COPY length, ADD head, verified)
+	const uint32_t* mem_s;     // per member slot (PairPlanDev::mem_base + chunk slots): epoch start
+	const uint32_t* n_mem;     // per chunk (PairPlanDev::chunk_base + c): members starting in it
+	const uint32_t* srec;      // per member slot: (x, COPY length, ADD head, verified)
+	const uint32_t* csum;      // per chunk: verified prefix length, its delta bytes
+	uint32_t* cmap;            // per chunk: member range taken in bulk -> record index (gathered after)
 };
 
-// Speculative diagonal members of the onepass chain (dg_members.hip).  The
-// member arrays share the record slots' indexing (rec_base + k): a closed
-// member spans >= p bytes, so K + 1 <= |V| / p + 1 = rec_cap.
-constexpr uint32_t kVerifyWaves = 8;   // verification waves per pair (64 members per pass)
+// Speculative diagonal members of the onepass chain (dg_members.hip): one
+// wave per chunk of kMemChunk positions, with kMemAhead bytes of look-ahead
+// staged for the members that end past the chunk.  Members start >= p = 16
+// bytes apart, so a chunk holds at most kMemChunk / 16 of them.
+constexpr uint32_t kMemChunk = 2048;
+constexpr uint32_t kMemAhead = 1024;
+constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
 
 struct SpecArgs {
 	const uint8_t* ref;
 	const uint8_t* ver;
 	const PairDev* pairs;
 	const PairPlanDev* pplan;
-	uint32_t n_pairs;
+	const uint2* chunks;       // per wave: (pair, chunk)
 	uint32_t* mem_s;           // per member slot: epoch start s_k
-	uint32_t* mem_x;           // per member slot: x_k, the step-T window (s_k + T_k)
-	uint32_t* n_mem;           // per pair: closed members K
-	uint32_t* srec;            // per member slot: (x, len, ADD head, verified)
+	uint32_t* n_mem;           // per chunk: members starting in it
+	uint32_t* srec;            // per member slot: (x, COPY length, ADD head, verified)
+	uint32_t* csum;            // per chunk: verified prefix length, its delta bytes
+	uint32_t* cmap;            // per chunk: (record index, first member, end member, -) to gather
 };
 
 // COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the
@@ -180,7 +190,8 @@ const char* ab_env(const char* name);
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
-hipError_t launch_members(const SpecArgs& a, hipStream_t st);
+hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, hipStream_t st);
+hipError_t launch_member_gather(const SpecArgs& a, uint32_t n_chunks, uint32_t* rec, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs

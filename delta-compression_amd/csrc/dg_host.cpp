@@ -330,7 +330,8 @@ struct dg_encode_plan {
 	// onepass member mode (dg_members.hip): member arrays share the record
 	// slots' indexing; the verification work queue
 	bool members = false;
-	DevBuf d_mem_s, d_mem_x, d_srec, d_nmem;
+	DevBuf d_mem_s, d_srec, d_nmem, d_chunks, d_csum, d_cmap;
+	uint32_t n_chunks = 0;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
@@ -531,10 +532,32 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		             !P->fused && want;
 	}
 	if (P->members) {
-		bad |= P->d_mem_s.alloc(4ull * std::max<uint64_t>(rec, 1));
-		bad |= P->d_mem_x.alloc(4ull * std::max<uint64_t>(rec, 1));
-		bad |= P->d_srec.alloc(16ull * std::max<uint64_t>(rec, 1));
-		bad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(n, 1));
+		// chunks of kMemChunk positions covering [0, min(|R|, |V|)]; member
+		// slots per chunk; the (pair, chunk) table the member kernel's waves index
+		std::vector<uint32_t> jobs;
+		uint64_t slots = 0;
+		for (uint32_t i = 0; i < n; ++i) {
+			const uint64_t E = std::min<uint64_t>(pairs[i].r_len, pairs[i].v_len);
+			const uint32_t nch = (uint32_t)(E / kMemChunk + 1);
+			P->pp[i].mem_base = slots;
+			P->pp[i].chunk_base = P->n_chunks;
+			P->pp[i].n_chunks = nch;
+			for (uint32_t c = 0; c < nch; ++c) {
+				jobs.push_back(i);
+				jobs.push_back(c);
+			}
+			slots += (uint64_t)nch * kMemChunkSlots;
+			P->n_chunks += nch;
+		}
+		bad |= P->d_mem_s.alloc(4ull * std::max<uint64_t>(slots, 1));
+		bad |= P->d_srec.alloc(16ull * std::max<uint64_t>(slots, 1));
+		bad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(P->n_chunks, 1));
+		bad |= P->d_chunks.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		bad |= P->d_csum.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		bad |= P->d_cmap.alloc(16ull * std::max<uint32_t>(P->n_chunks, 1));
+		if (!bad && !jobs.empty() &&
+		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
+			bad = 1;
 	}
 	if (bad) {
 		delete P;
@@ -590,6 +613,20 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t* P) { return P ? P->out_bound : 0; }
 uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t* P) { return P ? P->n : 0; }
 uint32_t dg_encode_plan_flags(const dg_encode_plan_t* P) { return P && P->members ? DG_PLAN_MEMBERS : 0u; }
+#ifdef DG_AB_SWITCHES
+// A/B and profiling builds only: the member kernel's outputs of the last run
+// (device pointers; scripts/member_debug.py)
+int dg_encode_plan_member_debug(const dg_encode_plan_t* P, void** mem_s, void** srec, void** n_mem,
+                                void** csum, uint32_t* n_chunks) {
+	if (!P || !P->members) return -1;
+	*mem_s = P->d_mem_s.p;
+	*srec = P->d_srec.p;
+	*n_mem = P->d_nmem.p;
+	*csum = P->d_csum.p;
+	*n_chunks = P->n_chunks;
+	return 0;
+}
+#endif
 uint64_t dg_encode_plan_table_size(const dg_encode_plan_t* P, uint32_t i) {
 	return (P && i < P->n) ? P->pp[i].q : 0;
 }
@@ -720,17 +757,28 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				m.ver = d_ver;
 				m.pairs = a.pairs;
 				m.pplan = a.pplan;
-				m.n_pairs = P->n;
+				m.chunks = P->d_chunks.as<uint2>();
 				m.mem_s = P->d_mem_s.as<uint32_t>();
-				m.mem_x = P->d_mem_x.as<uint32_t>();
 				m.n_mem = P->d_nmem.as<uint32_t>();
 				m.srec = P->d_srec.as<uint32_t>();
-				HIPCHK(ctx, launch_members(m, st));
+				m.csum = P->d_csum.as<uint32_t>();
+				m.cmap = P->d_cmap.as<uint32_t>();
+				HIPCHK(ctx, launch_members(m, P->n_chunks, st));
+				a.csum = m.csum;
+				a.cmap = m.cmap;
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
 			}
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
+			if (P->members) {   // the members the chain took in bulk, into the record arrays
+				SpecArgs m{};
+				m.pplan = a.pplan;
+				m.chunks = P->d_chunks.as<uint2>();
+				m.srec = P->d_srec.as<uint32_t>();
+				m.cmap = P->d_cmap.as<uint32_t>();
+				HIPCHK(ctx, launch_member_gather(m, P->n_chunks, a.rec, st));
+			}
 		} else {
 			// fresh R indexes (~0 = empty slot), then build + scan
 			a.ctab = P->d_ctab.as<uint32_t>();

@@ -62,8 +62,11 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #ifdef DG_ONEPASS_PROF
 enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATCH, P_B_ENTRIES,
        P_B_CHUNKS, P_C_CHUNKS, P_EXTENDS, P_REFILLS, P_T_DIAG, P_T_A, P_T_BC, P_T_EXT, P_T_REFILL,
-       P_T_TOTAL, P_B_WALKED, P_T_D1, P_T_D2, P_T_D3, P_T_D4, P_D_MEMBERS, P_D_STEPS, P_T_D3A, P_T_D3B, kProfN };
+       P_T_TOTAL, P_B_WALKED, P_T_D1, P_T_D2, P_T_D3, P_T_D4, P_D_MEMBERS, P_D_STEPS, P_T_D3A, P_T_D3B,
+       P_T_TAKE, P_T_RESYNC, P_TAKES, P_RESYNCS, P_T_FINAL, kProfN };
 __device__ unsigned long long g_onepass_prof[kProfN];
+constexpr uint32_t kPairProfMax = 16384;   // per pair: start, end (realtime), t_bc, exact epochs
+__device__ unsigned long long g_pair_prof[kPairProfMax * 4];
 #define PROF_DECL uint64_t prof[kProfN];
 #define PROF_INIT(o) for (int _i = 0; _i < kProfN; ++_i) (o).prof[_i] = 0;
 #ifdef DG_ONEPASS_PROF_LITE   // only the refill wait, the epoch counts and the total are timed
@@ -692,6 +695,16 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	uint32_t tag = 0;
 	unsigned long long* HV = nullptr;
 	unsigned long long* HR = nullptr;
+	// the epoch's last tag goes back with the table, so its next holder
+	// starts above every entry this one wrote
+	auto release_table = [&]() {
+		if (lane == 0) {
+			__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			vm_drain();
+			__hip_atomic_store(&a.table_locks[tslot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		tslot = -1;
+	};
 
 	uint32_t v0 = 0, r0 = 0;
 	bool scanning = vl > 0;
@@ -699,22 +712,57 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	bool skipA = false;         // the epoch is known to be long: phase B from step 0
 
 	// ── member mode (dg_members.hip): verified diagonal members are taken as
-	//    they are, 64 records per pass; the epochs below run only from an
-	//    unverified member until the chain lands on a later member start, and
-	//    for the final epoch ──
+	//    they are, 64 records per pass, chunk after chunk; the epochs below
+	//    run only from an unverified member until the chain lands on a later
+	//    member start, and for the final epoch (whose member is never
+	//    verified: its run holds the end of the shorter stream) ──
 	const bool members = Src::kPhaseA && a.srec != nullptr;
-	uint32_t kmem = 0, Kmem = 0, s_cur = 0;
-	const uint32_t* msp = nullptr;
+	uint32_t kc = 0, ki = 0, nch = 0, cnt = 0, s_cur = 0;   // chunk, index in chunk, chunks, members in kc
+	const uint32_t* msp = nullptr;   // member starts of chunk 0 (chunk c: + c * kMemChunkSlots)
 	const uint32_t* srp = nullptr;
+	const uint32_t* ncp = nullptr;   // members per chunk
+	bool mem_live = false;           // members remain ahead of the chain
+	const uint32_t* csp = nullptr;   // per chunk: verified prefix, its delta bytes
+	uint32_t* cmp = nullptr;         // per chunk: bulk range -> record index (member_gather_kernel)
 	auto take_members = [&]() {
-		while (kmem < Kmem) {
-			const uint32_t n_in = umin32(Kmem - kmem, 64u);
-			const uint32_t j = kmem + lane;
+		[[maybe_unused]] const uint64_t tt0 = PROF_NOW();
+		if constexpr (Src::kPhaseA) PROF_ADD(src, P_TAKES, 1);
+		for (;;) {
+			if (kc >= nch) break;
+			if (ki == 0) {
+				// whole verified chunks from kc, 64 summaries at a time, go to
+				// the gather map; the first partial chunk contributes its
+				// verified prefix and stops the run
+				const uint32_t cj = kc + lane;
+				const bool inr = cj < nch;
+				const uint32_t cn = inr ? ncp[cj] : 0u;
+				const uint32_t vp = inr ? csp[2ull * cj] : 0u;
+				const uint32_t vb = inr ? csp[2ull * cj + 1] : 0u;
+				const uint64_t full = __ballot(inr && vp == cn);
+				const uint32_t nfull = full == ~0ull ? 64u : ffs64(~full);
+				const bool use = inr && lane <= nfull;
+				const uint32_t ct = use ? vp : 0u;   // == cn for the full chunks
+				const uint32_t incl = wave_incl_scan(ct);
+				const uint32_t tot = rdlane(incl, 63);
+				if (nrec + tot > rec_cap) { st = 7; scanning = false; return; }
+				if (use) *(uint4*)(cmp + 4ull * cj) = make_uint4(nrec + incl - ct, 0u, ct, 0u);
+				dsz += rdlane(wave_incl_scan(use ? vb : 0u), 63);
+				nrec += tot;
+				if (nfull == 64) { kc += 64; continue; }
+				kc += nfull;
+				if (kc >= nch) break;
+				cnt = uni(ncp[kc]);
+				ki = rdlane(vp, nfull);   // the first unverified member of chunk kc
+				break;
+			}
+			// mid-chunk, after a re-sync: records of the verified run copied here
+			const uint32_t n_in = umin32(cnt - ki, 64u);
+			const uint64_t slot = (uint64_t)kc * kMemChunkSlots + ki + lane;
 			uint4 r4 = make_uint4(0u, 0u, 0u, 0u);
 			uint32_t sj = 0;
 			if (lane < n_in) {
-				r4 = *(const uint4*)(srp + 4ull * j);
-				sj = msp[j];
+				r4 = *(const uint4*)(srp + 4ull * slot);
+				sj = msp[slot];
 			}
 			const uint64_t full = n_in == 64 ? ~0ull : ((1ull << n_in) - 1ull);
 			const uint64_t bad = ~__ballot(lane < n_in && r4.w != 0u) & full;
@@ -725,36 +773,55 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			const uint32_t sz = lane < take ? 13u + (gap ? 9u + gap : 0u) : 0u;
 			dsz += rdlane(wave_incl_scan(sz), 63);
 			nrec += take;
-			kmem += take;
-			if (take < n_in) break;   // member kmem is left to the epochs below
+			ki += take;
+			if (take < n_in) break;   // member (kc, ki) is left to the epochs below
+			if (ki >= cnt) { ++kc; ki = 0; }
 		}
-		s_cur = uni(msp[kmem]);
+		// the chain always ends on an unverified member (the final epoch's
+		// run holds the end of the shorter stream)
+		mem_live = kc < nch;
+		if (!mem_live) { st = 5; scanning = false; return; }
+		s_cur = uni(msp[(uint64_t)kc * kMemChunkSlots + ki]);
 		v0 = r0 = s_cur;
-		at_mismatch = kmem > 0;   // member starts past the first are mismatches
+		at_mismatch = kc != 0 || ki != 0;   // member starts past the first are mismatches
+		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_TAKE, PROF_NOW() - tt0);
 	};
 	if (members && scanning) {
-		Kmem = uni(a.n_mem[pair]);
-		msp = a.mem_s + pp.rec_base;
-		srp = a.srec + 4ull * pp.rec_base;
+		msp = a.mem_s + pp.mem_base;
+		srp = a.srec + 4ull * pp.mem_base;
+		ncp = a.n_mem + pp.chunk_base;
+		csp = a.csum + 2ull * pp.chunk_base;
+		cmp = a.cmap + 4ull * pp.chunk_base;
+		nch = uni(pp.n_chunks);
+		cnt = uni(ncp[0]);
 		take_members();
 	}
 
 	while (scanning) {
 		skipA = false;
-		if (members && kmem < Kmem && v0 == r0 && v0 > s_cur) {
-			// did the exact chain land on a later member start? (ascending)
-			uint32_t m = kmem + 1;
-			bool found = false;
-			while (m <= Kmem) {
-				const uint32_t j = m + lane;
-				const uint32_t sj = j <= Kmem ? msp[j] : 0xFFFFFFFFu;
-				const uint64_t eq = __ballot(sj == v0);
-				if (eq) { m += ffs64(eq); found = true; break; }
-				if (__ballot(sj > v0)) break;
-				m += 64;
+		if (members && mem_live && v0 == r0 && v0 > s_cur) {
+			[[maybe_unused]] const uint64_t tr0 = PROF_NOW();
+			if constexpr (Src::kPhaseA) PROF_ADD(src, P_RESYNCS, 1);
+			// did the exact chain land on a later member start? (ascending
+			// over the chunks)
+			uint32_t c2 = kc, i2 = ki + 1, n2 = cnt;
+			bool found = false, past = false;
+			while (!found && !past && c2 < nch) {
+				if (c2 != kc) n2 = uni(ncp[c2]);
+				for (; i2 < n2; i2 += 64) {
+					const uint32_t j = i2 + lane;
+					const uint32_t sj = j < n2 ? msp[(uint64_t)c2 * kMemChunkSlots + j] : 0xFFFFFFFFu;
+					const uint64_t eq = __ballot(sj == v0);
+					if (eq) { i2 += ffs64(eq); found = true; break; }
+					if (__ballot(j < n2 && sj > v0)) { past = true; break; }   // (not the padding lanes)
+				}
+				if (!found && !past) { ++c2; i2 = 0; }
 			}
+			if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_RESYNC, PROF_NOW() - tr0);
 			if (found) {
-				kmem = m;
+				kc = c2;
+				ki = i2;
+				cnt = n2;
 				take_members();
 				continue;
 			}
@@ -999,6 +1066,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			}
 		}
 		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_BC, PROF_NOW() - tb);
+		if (in_table) release_table();   // held for this epoch only: the pool serves the other waves
 		if (!matched) break;
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
@@ -1019,11 +1087,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	}
 	if (v0 < vl) dsz += 9 + (uint64_t)(vl - v0);   // trailing ADD (:268-275)
 
-	if (tslot >= 0 && lane == 0) {
-		__hip_atomic_store(&a.table_tags[tslot], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		vm_drain();
-		__hip_atomic_store(&a.table_locks[tslot], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-	}
+	if (tslot >= 0) release_table();
 	if (lane == 0) {
 		a.n_rec[pair] = nrec;
 		a.dsize[pair] = dsz;
@@ -1032,6 +1096,10 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 #ifdef DG_ONEPASS_PROF
 	if constexpr (Src::kPhaseA) {
 		PROF_ADD(src, P_EPOCHS, nrec);
+		if (lane == 0 && pair < kPairProfMax) {
+			g_pair_prof[4ull * pair + 2] = src.prof[P_T_BC];
+			g_pair_prof[4ull * pair + 3] = src.prof[P_DIAG_CALLS] + src.prof[P_A_ENTRIES] + 1000ull * src.prof[P_RESYNCS];
+		}
 		if (lane == 0)
 			for (int i = 0; i < kProfN; ++i) atomicAdd(&g_onepass_prof[i], (unsigned long long)src.prof[i]);
 	}
@@ -1059,6 +1127,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	src.powc = a.powc;
 	PROF_INIT(src)
 	[[maybe_unused]] const uint64_t t_start = PROF_NOW_R();
+#ifdef DG_ONEPASS_PROF
+	if (lane_id() == 0 && pair < kPairProfMax) g_pair_prof[4ull * pair] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1092,6 +1163,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	}
 #ifdef DG_ONEPASS_PROF
 	if (lane_id() == 0) atomicAdd(&g_onepass_prof[P_T_TOTAL], (unsigned long long)(PROF_NOW_R() - t_start));
+	if (lane_id() == 0 && pair < kPairProfMax) g_pair_prof[4ull * pair + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -1133,6 +1205,11 @@ extern "C" int dg_onepass_prof_read(unsigned long long* out, int n) {
 	if (n > kProfN) n = kProfN;
 	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_onepass_prof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
 	return n;
+}
+extern "C" int dg_onepass_pair_prof_read(unsigned long long* out, int n_pairs) {
+	if (n_pairs > (int)kPairProfMax) n_pairs = (int)kPairProfMax;
+	if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_prof), 32ull * n_pairs) != hipSuccess) return -1;
+	return n_pairs;
 }
 extern "C" int dg_onepass_prof_reset(void) {
 	unsigned long long z[kProfN] = {};

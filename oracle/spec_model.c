@@ -19,13 +19,16 @@
  *      x_k = (last mismatch of run k) + 1, matches there on the diagonal and
  *      extends to s_{k+1}.  The run holding the sentinel starts the final
  *      epoch s_K.
- *   2. A member is verified when (A) no V window of steps 0..T equals, in the
- *      low 32 fingerprint bits, an R window of another step of the member
- *      (then no lookup before T can verify, onepass.c:169-219), and (B) at
+ *   2. A member is verified when (A) no V window of steps 0..T equals, in a
+ *      32-bit equality-preserving hash (sm_hash, the kernels' win_hash), an R
+ *      window of another step of the member (only byte-equal windows can
+ *      verify a lookup, onepass.c:169-219), and (B) at
  *      T = x_k - s_k lookup 1 or lookup 2 finds step T itself as the slot's
  *      first writer of the epoch (onepass.c:141-166): slot_V(T) is not among
  *      slot_V(0..T-1), or slot_R(T) is not among slot_R(0..T-1); and
- *      T < SM_MAX_T.
+ *      T < SM_MAX_T, and the next member starts within SM_AHEAD bytes past
+ *      the end of the SM_CHUNK-byte chunk holding s_k (the kernel's staged
+ *      region).
  *   3. The chain takes verified members as they are; from an unverified one
  *      it runs the reference's epochs exactly until an epoch ends on diagonal
  *      0 at a later member start (re-sync), and the final epoch exactly.
@@ -36,7 +39,9 @@
 
 #include "delta_oracle.h"
 
-#define SM_MAX_T 256   /* members of T + 1 > 256 steps are left to the exact engine */
+#define SM_MAX_T 512   /* members of T + 1 > 512 steps are left to the exact engine */
+#define SM_CHUNK 2048  /* member_chunk_kernel: members belong to the chunk of their start ... */
+#define SM_AHEAD 1024  /* ... and need the next member's start within this look-ahead */
 
 typedef struct {
 	uint64_t members, verified, exact_epochs, resyncs;
@@ -107,19 +112,32 @@ static int sm_epoch(const uint8_t *r, size_t r_len, const uint8_t *v, size_t v_l
 	}
 }
 
+static uint32_t sm_rotr(uint32_t x, unsigned s) { return (x >> s) | (x << (32 - s)); }
+
+/* member_chunk_kernel's win_hash of the 16 bytes at d (little-endian words) */
+static uint32_t sm_hash(const uint8_t *d)
+{
+	uint32_t w[4];
+	memcpy(w, d, 16);
+	return w[0] ^ sm_rotr(w[1], 27) ^ sm_rotr(w[2], 21) ^ sm_rotr(w[3], 15);
+}
+
 /* (A) and (B) of the header for the member [s, x]. */
 static int sm_verify(const uint8_t *r, const uint8_t *v, size_t s, size_t x, size_t p, uint64_t q)
 {
 	const size_t T = x - s;
 	if (T + 1 > SM_MAX_T) return 0;
 	uint64_t fv[SM_MAX_T], fr[SM_MAX_T];
+	uint32_t hv[SM_MAX_T], hr[SM_MAX_T];
 	for (size_t t = 0; t <= T; ++t) {
 		fv[t] = or_fingerprint(v, s + t, p);
 		fr[t] = or_fingerprint(r, s + t, p);
+		hv[t] = sm_hash(v + s + t);
+		hr[t] = sm_hash(r + s + t);
 	}
 	for (size_t c = 0; c <= T; ++c)
 		for (size_t l = 0; l <= T; ++l)
-			if (c != l && (uint32_t)fv[c] == (uint32_t)fr[l]) return 0;
+			if (c != l && hv[c] == hr[l]) return 0;
 	int dup_v = 0, dup_r = 0;
 	for (size_t c = 0; c < T; ++c) {
 		if (fv[c] % q == fv[T] % q) dup_v = 1;
@@ -158,7 +176,9 @@ size_t sm_diff_onepass_spec(const uint8_t *r, size_t r_len, const uint8_t *v, si
 	/* 2. verification */
 	unsigned char *ok = calloc(K + 1, 1);
 	if (!ok) abort();
-	for (size_t k = 0; k < K; ++k) ok[k] = (unsigned char)sm_verify(r, v, ms[k], mx[k], p, q);
+	for (size_t k = 0; k < K; ++k)
+		ok[k] = (unsigned char)(ms[k + 1] < (ms[k] / SM_CHUNK + 1) * SM_CHUNK + SM_AHEAD &&
+		                        sm_verify(r, v, ms[k], mx[k], p, q));
 	st->members = K;
 	for (size_t k = 0; k < K; ++k) st->verified += ok[k];
 

@@ -16,13 +16,14 @@ sys.path.insert(0, ROOT)
 NAMES = ["epochs", "diag_calls", "diag_epochs", "diag_zero", "a_entries", "a_match", "b_entries",
          "b_chunks", "c_chunks", "extends", "refills", "t_diag", "t_a", "t_bc", "t_ext", "t_refill",
          "t_total", "b_walked", "t_d1_list", "t_d2_chain", "t_d3_fp_lookup", "t_d4_resolve", "d_members",
-         "d_steps", "t_d3a_map", "t_d3ab_map_fp"]
+         "d_steps", "t_d3a_map", "t_d3ab_map_fp", "t_take", "t_resync", "takes", "resyncs", "t_final"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
     ap.add_argument("--pairs", type=int, default=0)
+    ap.add_argument("--offset", type=int, default=0, help="first pair's index in the config's batch")
     args = ap.parse_args()
     os.environ.setdefault("DG_LIB_VARIANT", "prof")
     import torch
@@ -36,7 +37,7 @@ def main():
     n = args.pairs or npg
     ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    ctx.check(L_.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L, seed,
+    ctx.check(L_.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L, seed + args.offset,
                                             int(rate * L + 0.5), None), "synth")
     plan = dg.EncodePlan(ctx, "onepass", [(i * L, L, i * L, L) for i in range(n)], q=q)
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
@@ -53,6 +54,21 @@ def main():
     k = L_.dg_onepass_prof_read(buf, len(NAMES))
     vals = {NAMES[i]: buf[i] / n for i in range(k)}
     vals["stage_ms"] = plan.stage_times()
+    if hasattr(L_, "dg_onepass_pair_prof_read"):
+        import numpy as np
+        m = min(n, 16384)
+        pb = (C.c_ulonglong * (4 * m))()
+        L_.dg_onepass_pair_prof_read(pb, m)
+        a = np.frombuffer(pb, dtype=np.uint64).reshape(m, 4).astype(np.int64)
+        t0 = a[:, 0].min()
+        st_us, en_us = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0   # 100 MHz realtime
+        dur = en_us - st_us
+        order = np.argsort(-dur)[:8]
+        vals["pair_us"] = {"span": float(en_us.max()), "dur_p50": float(np.median(dur)),
+                           "dur_p99": float(np.percentile(dur, 99)), "dur_max": float(dur.max()),
+                           "start_p50": float(np.median(st_us)), "start_max": float(st_us.max()),
+                           "top": [[int(i), round(float(dur[i]), 1), round(float(st_us[i]), 1), int(a[i, 2]),
+                                    int(a[i, 3])] for i in order]}
     vals["pairs"] = n
     print(json.dumps({k2: (round(v, 2) if isinstance(v, float) else v) for k2, v in vals.items()}))
 

@@ -10,3 +10,4 @@ for c in c2 c3; do
   timeout -k 10 200 python bench.py --config $c --also none --steps 10 --warmup 2 --no-cpu-baseline > $O/$c.json 2> $O/$c.err || { echo "$c rc=$?"; tail -5 $O/$c.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/$c.json').read().strip().splitlines()[-1]); s=d['roofline']['stage_ms']; print('$c', d['value'], s)"
 done
+DG_MEMBERS=1 DG_LIB_VARIANT=prof timeout -k 10 120 python scripts/onepass_phases.py --config c3 > $O/c3.phases.json 2>&1 && tail -1 $O/c3.phases.json
