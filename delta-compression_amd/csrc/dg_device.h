@@ -106,7 +106,7 @@ struct EncodeArgs {
 // staged for the members that end past the chunk.  Members start >= p = 16
 // bytes apart, so a chunk holds at most kMemChunk / 16 of them.
 constexpr uint32_t kMemChunk = 2048;
-constexpr uint32_t kMemAhead = 1024;
+constexpr uint32_t kMemAhead = 1008;   // staged: [chunk - 16, chunk + 2048 + 1008) = 3 KiB
 constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
 
 struct SpecArgs {
@@ -190,7 +190,7 @@ const char* ab_env(const char* name);
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
-hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, hipStream_t st);
+hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 hipError_t launch_member_gather(const SpecArgs& a, uint32_t n_chunks, uint32_t* rec, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);

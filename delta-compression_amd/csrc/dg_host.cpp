@@ -763,7 +763,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				m.srec = P->d_srec.as<uint32_t>();
 				m.csum = P->d_csum.as<uint32_t>();
 				m.cmap = P->d_cmap.as<uint32_t>();
-				HIPCHK(ctx, launch_members(m, P->n_chunks, st));
+				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 				a.csum = m.csum;
 				a.cmap = m.cmap;
 				a.mem_s = m.mem_s;

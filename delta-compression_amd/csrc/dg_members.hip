@@ -41,6 +41,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dg_device.h"
 #include "dg_devutil.h"
 
@@ -51,7 +53,8 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr uint32_t kStage = kMemChunk + kMemAhead + 16;   // staged bytes per stream (lookbehind 16)
 constexpr uint32_t kMaskWords = (kStage + 31) / 32;        // mismatch bitmap words
 constexpr uint32_t kRunList = kStage / 17 + 4;             // run starts in the staged region (>= 17 apart)
-constexpr uint32_t kLongChunks = 8;                        // members of up to 512 steps are verified
+constexpr uint32_t kLongChunks = 8;
+constexpr uint32_t kMemWavesPerCu = 16;                    // persistent waves (LDS allows 17)                        // members of up to 512 steps are verified
 static_assert(kStage % 16 == 0, "16-byte blocks");
 
 // 16 mismatch bits of 16 bytes (bit i: byte i of the chunk differs)
@@ -76,27 +79,26 @@ __device__ __forceinline__ void lds_fence() {
 	__builtin_amdgcn_wave_barrier();
 }
 
-// Filters of a member set's steps other than their T steps (where V(T) ==
-// R(T) by construction): V window hashes, R window hashes, V slots.  A step
-// can fail (A) only if its R hash is in the first (or, at T, its V hash in
-// the second), and (B) only if the T step's V slot is in the third; the rare
-// flagged steps are resolved exactly with ballots.
+// Bloom filter of the V window hashes of a member set's steps other than
+// their T steps.  Check (A) splits by whether a pair of steps involves T:
+// V(T) == R(T) by construction (no mismatch in [x, x + 16)), so V(c) == R(T)
+// is V(c) == V(T) and V(T) == R(l) is R(T) == R(l), both plain ballots at T;
+// the other pairs (c, l != T) can exist only for an R hash in the filter, and
+// those rare flagged steps are resolved exactly with ballots.
 template <uint32_t W>
-struct MemberFilters {
-	uint32_t* f;   // 3 x W words
+struct VFilter {
+	uint32_t* f;   // W words
 	__device__ void clear() {
-		for (uint32_t i = lane_id(); i < 3 * W; i += 64) f[i] = 0u;
+		for (uint32_t i = lane_id(); i < W; i += 64) f[i] = 0u;
 	}
-	__device__ void add(uint32_t fVl, uint32_t fRl, uint32_t sV) {
-		bloom_add<W>(f, fVl);
-		bloom_add<W>(f + W, fRl);
-		bloom_add<W>(f + 2 * W, sV);
-	}
-	__device__ bool flagA(uint32_t fVl, uint32_t fRl, bool isT) const {
-		return bloom_has<W>(f, fRl) || (isT && bloom_has<W>(f + W, fVl));
-	}
-	__device__ bool flagB(uint32_t sV) const { return bloom_has<W>(f + 2 * W, sV); }
+	__device__ void add(uint32_t h) { bloom_add<W>(f, h); }
+	__device__ bool has(uint32_t h) const { return bloom_has<W>(f, h); }
 };
+
+// Intra-wave LDS hand-offs (lane A stores, lane B loads) need only program
+// order: a wave's LDS instructions execute in issue order, so a compiler
+// barrier replaces s_waitcnt + wave_barrier.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 struct ChunkLds {
 	uint8_t v[kStage + 16];   // + slack: the fifth dword of a window read
@@ -105,43 +107,155 @@ struct ChunkLds {
 	uint32_t last[kMaskWords];   // max mismatch offset + 1 over words <= j (0: none)
 	uint16_t run[kRunList];      // run starts (offsets), ascending
 	uint32_t mark[64];
-	uint32_t filt[3 * 256];      // member filters: short rounds 3 x 64 words, long members 3 x 256
+	uint32_t filt[256];          // V-hash filter: short rounds 64 words, long members 64 / 256
 	uint8_t ok[kMemChunkSlots];  // per member of the chunk: verified
 	uint16_t sz[kMemChunkSlots]; // per member: its ADD + COPY bytes in the delta
 };
 
-// the 16 bytes at offset o of a staged stream, as little-endian words
-__device__ __forceinline__ void win16(const uint8_t* s, uint32_t o, uint32_t (&w)[4]) {
-	const uint32_t* d = (const uint32_t*)(s + (o & ~3u));
-	const uint32_t sh = o & 3u;
-	const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
-	w[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-	w[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
-	w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
-	w[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
+// the 16 bytes at offset o of a staged stream: one unaligned ds_read_b128
+// (gfx950 runs with unaligned LDS access)
+__device__ __forceinline__ uint4 lds16(const uint8_t* s, uint32_t o) {
+	uint4 w;
+	__builtin_memcpy(&w, s + o, 16);
+	return w;
 }
 
 // An equality-preserving 32-bit hash of a window for check (A): only byte-
 // equal windows can make a lookup verify (memcmp, onepass.c:186,212), so
 // equal windows must hash equal; unequal ones that collide only make the
 // check conservative.  Six VALU ops instead of a second fingerprint.
-__device__ __forceinline__ uint32_t win_hash(const uint32_t (&w)[4]) {
-	return w[0] ^ __builtin_amdgcn_alignbit(w[1], w[1], 27) ^ __builtin_amdgcn_alignbit(w[2], w[2], 21) ^
-	       __builtin_amdgcn_alignbit(w[3], w[3], 15);
+__device__ __forceinline__ uint32_t win_hash(const uint4& w) {
+	return w.x ^ __builtin_amdgcn_alignbit(w.y, w.y, 27) ^ __builtin_amdgcn_alignbit(w.z, w.z, 21) ^
+	       __builtin_amdgcn_alignbit(w.w, w.w, 15);
 }
 
-__device__ __forceinline__ uint64_t fp_lds(const uint8_t* s, uint32_t o, uint32_t& w0) {
-	uint32_t w[4];
-	win16(s, o, w);
-	w0 = w[0];
-	return fp16_dot(w[0], w[1], w[2], w[3]);
+__device__ __forceinline__ uint32_t slot_lds(const uint8_t* s, uint32_t o, const ModQ& mq, uint64_t q, uint64_t qmag) {
+	const uint4 w = lds16(s, o);
+	return slot_of(fp16_dot(w.x, w.y, w.z, w.w), mq, q, qmag);
 }
 
-__global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
-	__shared__ __attribute__((aligned(16))) ChunkLds L;
+// lanes [a, b) (a <= b <= 64)
+__device__ __forceinline__ uint64_t lanes_range(uint32_t a, uint32_t b) {
+	const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1ull);
+	return hi & ~((1ull << a) - 1ull);
+}
+
+// One long member (64 <= T < 64 kLongChunks) at staged offset s0: 64 steps
+// per lane row, history in VGPRs, W-word filters.  Returns its verdict.
+template <uint32_t W>
+__device__ __forceinline__ bool long_member_ok(const uint8_t* SV, const uint8_t* SR, uint32_t s0, uint32_t tl,
+                                               uint32_t* filt, const ModQ& mq, uint64_t q, uint64_t qmag,
+                                               uint32_t& pw) {
 	const uint32_t lane = lane_id();
-	const uint2 job = a.chunks[blockIdx.x];   // (pair, chunk)
-	const uint32_t pair = job.x, c = job.y;
+	const uint32_t C = tl / 64 + 1, CT = tl / 64, LT = tl % 64;
+	VFilter<W> fl{filt};
+	uint32_t hsV[kLongChunks], hfV[kLongChunks], hfR[kLongChunks];   // V slots, V / R window hashes
+	lds_order();
+	fl.clear();
+	lds_order();
+	pw = 0;
+#pragma unroll
+	for (uint32_t cc = 0; cc < kLongChunks; ++cc) {
+		hsV[cc] = kSentinel;
+		hfV[cc] = 0u;
+		hfR[cc] = 1u;
+		const uint32_t t = 64 * cc + lane;
+		if (cc < C && t <= tl) {
+			const uint4 wv = lds16(SV, s0 + t), wr = lds16(SR, s0 + t);
+			hsV[cc] = slot_of(fp16_dot(wv.x, wv.y, wv.z, wv.w), mq, q, qmag);
+			hfV[cc] = win_hash(wv);
+			hfR[cc] = win_hash(wr);
+			if (cc == 0) pw = wv.x;
+			if (t != tl) fl.add(hfV[cc]);
+		}
+	}
+	pw = rdlane(pw, 0);
+	lds_order();
+	bool bad = false;
+	// (A) through T: V(c) == V(T) or R(l) == R(T) for a step before T
+	uint32_t hT = 0, vT = 0;
+#pragma unroll
+	for (uint32_t cc = 0; cc < kLongChunks; ++cc)
+		if (cc == CT) {
+			hT = rdlane(hfV[cc], LT);
+			vT = rdlane(hsV[cc], LT);
+		}
+#pragma unroll
+	for (uint32_t c2 = 0; c2 < kLongChunks; ++c2)
+		if (c2 <= CT)
+			bad = bad || (__ballot(hfV[c2] == hT || hfR[c2] == hT) & (c2 < CT ? ~0ull : lanes_range(0, LT))) != 0;
+	// (A) off T: flagged steps' R hashes against every other step's V hash
+#pragma unroll
+	for (uint32_t cc = 0; cc < kLongChunks; ++cc) {
+		if (cc < C) {
+			const uint32_t t = 64 * cc + lane;
+			for (uint64_t w = __ballot(t < tl && fl.has(hfR[cc])); w && !bad; w &= w - 1) {
+				const uint32_t Lx = ffs64(w);
+				const uint32_t fR = rdlane(hfR[cc], Lx);
+#pragma unroll
+				for (uint32_t c2 = 0; c2 < kLongChunks; ++c2) {
+					if (c2 < C) {
+						const bool other = 64 * c2 + lane <= tl && !(c2 == cc && lane == Lx);
+						if (__ballot(other && hfV[c2] == fR)) bad = true;
+					}
+				}
+			}
+		}
+	}
+	if (bad) return false;
+	// (B): the T step's V slot against the earlier V slots; R slots only when
+	// it repeats
+	bool d1 = false;
+#pragma unroll
+	for (uint32_t c2 = 0; c2 < kLongChunks; ++c2)
+		if (c2 <= CT) d1 = d1 || (__ballot(hsV[c2] == vT) & (c2 < CT ? ~0ull : lanes_range(0, LT))) != 0;
+	if (!d1) return true;
+	const uint32_t rT = slot_lds(SR, s0 + tl, mq, q, qmag);
+	bool d2 = false;
+	for (uint32_t c2 = 0; c2 <= CT; ++c2) {
+		const uint32_t t2 = 64 * c2 + lane;
+		const uint32_t sr2 = t2 < tl ? slot_lds(SR, s0 + t2, mq, q, qmag) : kSentinel;
+		d2 = d2 || __ballot(t2 < tl && sr2 == rT) != 0;
+	}
+	return !d2;
+}
+
+// the staged region of one chunk in VGPRs (16 bytes per lane per row), loaded
+// while the previous chunk is verified
+constexpr uint32_t kStageRows = kStage / 1024;
+static_assert(kStage % 1024 == 0, "whole rows");
+struct StageRegs {
+	uint4 v[kStageRows], r[kStageRows];
+};
+
+// 16 bytes of a stream at p (16-aligned; bytes at or past len read as 0)
+__device__ __forceinline__ uint4 load16_tail(const uint8_t* S, int64_t p, uint32_t len) {
+	if (p < 0 || p >= (int64_t)len) return make_uint4(0u, 0u, 0u, 0u);
+	if (p + 16 <= (int64_t)len) return *(const uint4*)(S + p);
+	uint32_t w[4] = {0u, 0u, 0u, 0u};
+	for (uint32_t b = 0; p + b < (int64_t)len; ++b) w[b >> 2] |= (uint32_t)S[p + b] << (8 * (b & 3u));
+	return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void stage_load(const SpecArgs& a, uint32_t job, StageRegs& S) {
+	const uint2 jb = a.chunks[job];
+	const PairDev pd = a.pairs[jb.x];
+	const int64_t g0 = (int64_t)jb.y * kMemChunk - 16;
+	const uint8_t* V = a.ver + pd.v_off;
+	const uint8_t* R = a.ref + pd.r_off;
+	const uint32_t lane = lane_id();
+#pragma unroll
+	for (uint32_t k = 0; k < kStageRows; ++k) {
+		const int64_t p = g0 + 1024 * k + 16 * lane;
+		S.v[k] = load16_tail(V, p, (uint32_t)pd.v_len);
+		S.r[k] = load16_tail(R, p, (uint32_t)pd.r_len);
+	}
+}
+
+__device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uint32_t job) {
+	const uint32_t lane = lane_id();
+	const uint2 jb = a.chunks[job];   // (pair, chunk)
+	const uint32_t pair = jb.x, c = jb.y;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
@@ -150,22 +264,6 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
 	const int64_t g0 = (int64_t)cw - 16;                // position of staged offset 0
 	const uint64_t slot0 = pp.mem_base + (uint64_t)c * kMemChunkSlots;
 
-	// ── 1. stage [g0, g0 + kStage) of both streams (positions >= 0, < E) ──
-	{
-		const uint8_t* V = a.ver + pd.v_off;
-		const uint8_t* R = a.ref + pd.r_off;
-#pragma unroll
-		for (uint32_t k = 0; k < (kStage + 1023) / 1024; ++k) {
-			const uint32_t o = 1024 * k + 16 * lane;
-			const int64_t p = g0 + (int64_t)o;
-			if (o < kStage && p >= 0 && p < (int64_t)E) {
-				__builtin_amdgcn_global_load_lds((const void*)(V + p), (lds_void_t*)(L.v + 1024 * k), 16, 0, 0);
-				__builtin_amdgcn_global_load_lds((const void*)(R + p), (lds_void_t*)(L.r + 1024 * k), 16, 0, 0);
-			}
-		}
-		vm_drain();
-		__syncthreads();
-	}
 	// ── 2. mismatch bitmap: bit o = position g0 + o differs (or is E, the
 	//    sentinel); chunk 0's lookbehind holds only the virtual mismatch at -1 ──
 	const int64_t lim = (int64_t)E - g0;   // offset of the sentinel
@@ -225,8 +323,7 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
 
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
 	const ModQ mq = make_modq(q, qmag);
-	MemberFilters<64> fs{L.filt};
-	MemberFilters<256> fl{L.filt};
+	VFilter<64> fs{L.filt};
 	const uint8_t* SV = L.v;
 	const uint8_t* SR = L.r;
 
@@ -264,70 +361,84 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
 			const bool in = shrt && P > done && P <= done + 64;
 			const uint64_t RM = __ballot(in);
 			if (!RM) break;
+#ifdef DG_MEM_SKIP_SHORT   // timing variants only
+			break;
+#endif
 			const uint32_t hi = 63u - (uint32_t)__builtin_clzll(RM);
 			const uint32_t B = rdlane(P, hi) - done;   // live steps of the round
 			// lane -> member: a mark at each member's first step, prefix max
-			__builtin_amdgcn_wave_barrier();
+			lds_order();
 			L.mark[lane] = 0u;
 			fs.clear();
-			lds_fence();
+			lds_order();
 			const uint32_t st = P - (T + 1) - done;   // first step lane (members in the round)
 			if (in) L.mark[st] = lane + 1u;
-			lds_fence();
+			lds_order();
 			const bool live = lane < B;
 			const uint32_t mk = wave_incl_max(L.mark[lane]);   // lane 0 always holds a mark
 			const uint32_t mj = live ? mk - 1u : 0u;            // member lane
-			const uint32_t ms_j = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)s);
-			const uint32_t mt_j = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)T);
-			const uint32_t fb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)st);
-			const uint32_t snj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)sn);
+			// (start, T, first step lane) of this lane's member, one bpermute
+			const uint32_t inf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)(s | (T << 12) | (st << 18)));
+			const uint32_t ms_j = inf & 0xFFFu, mt_j = (inf >> 12) & 63u, fb = inf >> 18;
 			const uint32_t t = lane - fb;
 			const bool isT = live && t == mt_j;
 			uint32_t sV = kSentinel, fVl = 0, fRl = 1, w0 = 0;   // (fVl, fRl: window hashes)
 			if (live) {
-				uint32_t wv[4], wr[4];
-				win16(SV, ms_j + t, wv);
-				win16(SR, ms_j + t, wr);
-				sV = slot_of(fp16_dot(wv[0], wv[1], wv[2], wv[3]), mq, q, qmag);
+				const uint4 wv = lds16(SV, ms_j + t), wr = lds16(SR, ms_j + t);
+#ifdef DG_MEM_SKIP_FP   // timing variants only: no fingerprints
+				sV = wv.x % 16411u;
+#else
+				sV = slot_of(fp16_dot(wv.x, wv.y, wv.z, wv.w), mq, q, qmag);
+#endif
 				fVl = win_hash(wv);
 				fRl = win_hash(wr);
-				w0 = wv[0];
+				w0 = wv.x;
 			}
-			if (live && !isT) fs.add(fVl, fRl, sV);
-			lds_fence();
+#ifndef DG_MEM_SKIP_A
+			if (live && !isT) fs.add(fVl);
+#endif
+			lds_order();
 			const uint64_t mem = live ? lanes_mask(fb, mt_j + 1) : 0ull;   // this lane's member
 			bool bad = false;
-			// (A): steps with an off-diagonal equal-window candidate
-			for (uint64_t w = __ballot(live && fs.flagA(fVl, fRl, isT)); w; w &= w - 1) {
+			// (A) off T: steps whose R hash may equal another step's V hash
+#ifdef DG_MEM_SKIP_A
+			for (uint64_t w = 0; w; w &= w - 1) {
+#else
+			for (uint64_t w = __ballot(live && !isT && fs.has(fRl)); w; w &= w - 1) {
+#endif
 				const uint32_t Lx = ffs64(w);
 				const uint64_t others = ((uint64_t)rdlane((uint32_t)(mem >> 32), Lx) << 32 | rdlane((uint32_t)mem, Lx)) &
 				                        ~(1ull << Lx);
-				bool hit = (__ballot(fVl == rdlane(fRl, Lx)) & others) != 0;
-				if (rdlane(isT ? 1u : 0u, Lx)) hit = hit || (__ballot(fRl == rdlane(fVl, Lx)) & others) != 0;
+				const bool hit = (__ballot(fVl == rdlane(fRl, Lx)) & others) != 0;
 				bad = bad || (hit && lane == Lx);
 			}
-			// (B): T steps whose V slot may repeat an earlier V slot of the
-			// member; R slots (needed only then) are computed on demand
+			// T steps: (A) through T (a V or R repeat of the T window among the
+			// member's earlier steps), then (B) — the T step's V slot against
+			// the earlier V slots, R slots computed on demand
 			uint32_t sR = kSentinel - 1u;
 			bool have_sR = false;
-			for (uint64_t w = __ballot(isT && fs.flagB(sV)); w; w &= w - 1) {
-				const uint32_t Lx = ffs64(w);
-				const uint64_t before = ((uint64_t)rdlane((uint32_t)(mem >> 32), Lx) << 32 | rdlane((uint32_t)mem, Lx)) &
-				                        ((1ull << Lx) - 1ull);
-				const bool d1 = (__ballot(sV == rdlane(sV, Lx)) & before) != 0;
-				if (d1 && !have_sR) {
-					uint32_t dummy;
-					if (live) sR = slot_of(fp_lds(SR, ms_j + t, dummy), mq, q, qmag);
+			for (uint64_t w = __ballot(isT); w; w &= w - 1) {
+				const uint32_t LT = ffs64(w);
+				const uint64_t before = lanes_range(rdlane(fb, LT), LT);
+				const uint32_t hT = rdlane(fVl, LT);
+				if ((__ballot(fVl == hT || fRl == hT) & before) != 0) {
+					bad = bad || lane == LT;
+					continue;
+				}
+				if ((__ballot(sV == rdlane(sV, LT)) & before) == 0) continue;
+				if (!have_sR) {
+					if (live) sR = slot_lds(SR, ms_j + t, mq, q, qmag);
 					have_sR = true;
 				}
-				const bool d2 = d1 && (__ballot(sR == rdlane(sR, Lx)) & before) != 0;
-				bad = bad || (d2 && lane == Lx);
+				const bool d2 = (__ballot(sR == rdlane(sR, LT)) & before) != 0;
+				bad = bad || (d2 && lane == LT);
 			}
 			// verdict at each member's T step; the record carries the ADD head
 			// (the first step's V window) and the COPY length
 			const uint64_t BA = __ballot(bad);
 			const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fb << 2), (int)w0);
 			if (isT) {
+				const uint32_t snj = L.run[k0 + mj + 1];
 				const uint32_t xx = (uint32_t)(g0 + (int64_t)(ms_j + mt_j));
 				const uint32_t v = (BA & mem) == 0 ? 1u : 0u;
 				*(uint4*)(srec + 4 * mj) = make_uint4(xx, snj - (ms_j + mt_j), pw, v);
@@ -336,84 +447,21 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
 			done += B;
 		}
 
-		// ── long members (64 <= T < 512): 64-step chunks, history in VGPRs ──
+		// ── long members (64 <= T < 512): 64-step rows, history in VGPRs ──
+#ifdef DG_MEM_SKIP_LONG   // timing variants only
+		for (uint64_t LM = 0; LM; LM &= LM - 1) {
+#else
 		for (uint64_t LM = __ballot(known && !shrt && T < 64u * kLongChunks); LM; LM &= LM - 1) {
+#endif
 			const uint32_t M = ffs64(LM);
 			const uint32_t s0 = rdlane(s, M), tl = rdlane(T, M), sn0 = rdlane(sn, M);
-			const uint32_t C = tl / 64 + 1;   // chunks
-			uint32_t hsV[kLongChunks], hfV[kLongChunks], hfR[kLongChunks];   // V slots, V / R window hashes
-			uint32_t pw = 0;
-			__builtin_amdgcn_wave_barrier();
-			fl.clear();
-			lds_fence();
-#pragma unroll
-			for (uint32_t cc = 0; cc < kLongChunks; ++cc) {
-				hsV[cc] = kSentinel;
-				hfV[cc] = 0u;
-				hfR[cc] = 1u;
-				const uint32_t t = 64 * cc + lane;
-				if (cc < C && t <= tl) {
-					uint32_t wv[4], wr[4];
-					win16(SV, s0 + t, wv);
-					win16(SR, s0 + t, wr);
-					hsV[cc] = slot_of(fp16_dot(wv[0], wv[1], wv[2], wv[3]), mq, q, qmag);
-					hfV[cc] = win_hash(wv);
-					hfR[cc] = win_hash(wr);
-					if (cc == 0) pw = wv[0];
-					if (t != tl) fl.add(hfV[cc], hfR[cc], hsV[cc]);
-				}
-			}
-			pw = rdlane(pw, 0);
-			lds_fence();
-			bool bad = false;
-#pragma unroll
-			for (uint32_t cc = 0; cc < kLongChunks; ++cc) {
-				if (cc < C) {
-					const uint32_t t = 64 * cc + lane;
-					const bool stp = t <= tl, isT = t == tl;
-					// (A)
-					for (uint64_t w = __ballot(stp && fl.flagA(hfV[cc], hfR[cc], isT)); w && !bad; w &= w - 1) {
-						const uint32_t Lx = ffs64(w);
-						const uint32_t fR = rdlane(hfR[cc], Lx), fV = rdlane(hfV[cc], Lx);
-						const bool atT = 64 * cc + Lx == tl;
-#pragma unroll
-						for (uint32_t c2 = 0; c2 < kLongChunks; ++c2) {
-							if (c2 < C) {
-								const bool other = 64 * c2 + lane <= tl && !(c2 == cc && lane == Lx);
-								if (__ballot(other && (hfV[c2] == fR || (atT && hfR[c2] == fV)))) bad = true;
-							}
-						}
-					}
-					// (B), R slots recomputed only when the V slot repeats
-					if (__ballot(isT && fl.flagB(hsV[cc])) && !bad) {
-						const uint32_t LT = tl % 64;
-						const uint32_t vT = rdlane(hsV[cc], LT);
-						bool d1 = false;
-#pragma unroll
-						for (uint32_t c2 = 0; c2 < kLongChunks; ++c2) {
-							if (c2 <= cc) {
-								const uint64_t below = c2 < cc ? ~0ull : ((1ull << LT) - 1ull);
-								d1 = d1 || (__ballot(hsV[c2] == vT) & below) != 0;
-							}
-						}
-						if (d1) {
-							uint32_t dummy;
-							const uint32_t rT = slot_of(fp_lds(SR, s0 + tl, dummy), mq, q, qmag);
-							bool d2 = false;
-							for (uint32_t c2 = 0; c2 <= cc; ++c2) {
-								const uint32_t t2 = 64 * c2 + lane;
-								const uint32_t sr2 = t2 < tl ? slot_of(fp_lds(SR, s0 + t2, dummy), mq, q, qmag) : kSentinel;
-								d2 = d2 || __ballot(t2 < tl && sr2 == rT) != 0;
-							}
-							bad = d2;
-						}
-					}
-				}
-			}
+			uint32_t pw;
+			const bool ok = tl < 128 ? long_member_ok<64>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw)
+			                         : long_member_ok<256>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw);
 			if (lane == 0) {
 				*(uint4*)(srec + 4 * M) = make_uint4((uint32_t)(g0 + (int64_t)(s0 + tl)), sn0 - (s0 + tl), pw,
-				                                     bad ? 0u : 1u);
-				L.ok[k0 + M] = bad ? 0u : 1u;
+				                                     ok ? 1u : 0u);
+				L.ok[k0 + M] = ok ? 1u : 0u;
 			}
 		}
 	}
@@ -441,6 +489,29 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a) {
 	}
 }
 
+// Persistent waves over contiguous runs of chunks (the look-ahead a chunk
+// shares with the next one stays in this XCD's L2): the next chunk's bytes
+// are loaded into VGPRs while this one is verified, so no wave waits on HBM.
+__global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a, uint32_t n_chunks) {
+	__shared__ __attribute__((aligned(16))) ChunkLds L;
+	const uint32_t lane = lane_id();
+	const uint32_t j0 = (uint32_t)((uint64_t)n_chunks * blockIdx.x / gridDim.x);
+	const uint32_t j1 = (uint32_t)((uint64_t)n_chunks * (blockIdx.x + 1) / gridDim.x);
+	StageRegs S;
+	if (j0 < j1) stage_load(a, j0, S);
+	for (uint32_t j = j0; j < j1; ++j) {
+		lds_order();   // the previous chunk's LDS reads are issued
+#pragma unroll
+		for (uint32_t k = 0; k < kStageRows; ++k) {
+			*(uint4*)(L.v + 1024 * k + 16 * lane) = S.v[k];
+			*(uint4*)(L.r + 1024 * k + 16 * lane) = S.r[k];
+		}
+		lds_order();
+		if (j + 1 < j1) stage_load(a, j + 1, S);
+		member_chunk(a, L, j);
+	}
+}
+
 // Copies every chunk's taken member records (the chain kernel's map: record
 // index, first and end member) into the pair's record array as (x, x, len,
 // ADD head) onepass records.
@@ -458,9 +529,10 @@ __global__ __launch_bounds__(64) void member_gather_kernel(SpecArgs a, uint32_t*
 	}
 }
 
-hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, hipStream_t st) {
+hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {
 	if (n_chunks == 0) return hipSuccess;
-	hipLaunchKernelGGL(member_chunk_kernel, dim3(n_chunks), dim3(64), 0, st, a);
+	const uint32_t waves = std::min<uint32_t>(n_chunks, kMemWavesPerCu * std::max(n_cu, 1u));
+	hipLaunchKernelGGL(member_chunk_kernel, dim3(waves), dim3(64), 0, st, a, n_chunks);
 	return hipGetLastError();
 }
 
