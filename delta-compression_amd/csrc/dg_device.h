@@ -98,8 +98,17 @@ struct EncodeArgs {
 	const uint32_t* n_mem;     // per chunk (PairPlanDev::chunk_base + c): members starting in it
 	const uint32_t* srec;      // per member slot: (x, COPY length, ADD head, verified)
 	const uint32_t* csum;      // per chunk: verified prefix length, its delta bytes
-	uint32_t* cmap;            // per chunk: member range taken in bulk -> record index (gathered after)
+	// the delta's pieces for member_serialize_kernel: per chunk (chunk_base +
+	// c) the members taken in bulk (count, byte offset in the delta; zeroed by
+	// the member kernel), and per pair (n_chunks + 2 entries from chunk_base +
+	// 2 pair) the runs of records the chain wrote itself, then the trailing
+	// ADD + END: uint4 (first record or kSegTail, count, byte offset, ADD start)
+	uint32_t* cmap;
+	uint32_t* seg;
+	uint32_t* nseg;            // per pair: segments written
 };
+
+constexpr uint32_t kSegTail = 0xFFFFFFFFu;
 
 // Speculative diagonal members of the onepass chain (dg_members.hip): one
 // wave per chunk of kMemChunk positions, with kMemAhead bytes of look-ahead
@@ -119,7 +128,26 @@ struct SpecArgs {
 	uint32_t* n_mem;           // per chunk: members starting in it
 	uint32_t* srec;            // per member slot: (x, COPY length, ADD head, verified)
 	uint32_t* csum;            // per chunk: verified prefix length, its delta bytes
-	uint32_t* cmap;            // per chunk: (record index, first member, end member, -) to gather
+	uint32_t* cmap;            // per chunk: bulk (count, byte offset), zeroed here
+};
+
+// member-mode serialisation (dg_members.hip): one wave per (pair, chunk) job
+// writes the pair's segments 2c, 2c + 1 (the last chunk's wave the rest)
+struct MemSerArgs {
+	const uint8_t* ver;
+	const PairDev* pairs;
+	const PairPlanDev* pplan;
+	const uint2* chunks;
+	const uint32_t* cmap;
+	const uint32_t* seg;
+	const uint32_t* nseg;
+	const uint32_t* mem_s;
+	const uint32_t* srec;
+	const uint32_t* rec;       // kRecWordsOnepass words per record
+	const uint64_t* offsets;   // n + 1
+	uint8_t* out;
+	uint64_t out_cap;
+	int32_t* status;
 };
 
 // COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the
@@ -191,7 +219,7 @@ const char* ab_env(const char* name);
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
-hipError_t launch_member_gather(const SpecArgs& a, uint32_t n_chunks, uint32_t* rec, hipStream_t st);
+hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs

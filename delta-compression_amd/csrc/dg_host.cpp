@@ -330,7 +330,7 @@ struct dg_encode_plan {
 	// onepass member mode (dg_members.hip): member arrays share the record
 	// slots' indexing; the verification work queue
 	bool members = false;
-	DevBuf d_mem_s, d_srec, d_nmem, d_chunks, d_csum, d_cmap;
+	DevBuf d_mem_s, d_srec, d_nmem, d_chunks, d_csum, d_cmap, d_seg, d_nseg;
 	uint32_t n_chunks = 0;
 	uint32_t n_crc_spans = 0, n_crc_segs = 0;
 	// fork/join of the CRC kernels onto a side stream
@@ -554,7 +554,9 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		bad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(P->n_chunks, 1));
 		bad |= P->d_chunks.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
 		bad |= P->d_csum.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
-		bad |= P->d_cmap.alloc(16ull * std::max<uint32_t>(P->n_chunks, 1));
+		bad |= P->d_cmap.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		bad |= P->d_seg.alloc(16ull * ((uint64_t)P->n_chunks + 2ull * n));
+		bad |= P->d_nseg.alloc(4ull * std::max<uint32_t>(n, 1));
 		if (!bad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
 			bad = 1;
@@ -766,19 +768,13 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 				a.csum = m.csum;
 				a.cmap = m.cmap;
+				a.seg = P->d_seg.as<uint32_t>();
+				a.nseg = P->d_nseg.as<uint32_t>();
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
 			}
 			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
-			if (P->members) {   // the members the chain took in bulk, into the record arrays
-				SpecArgs m{};
-				m.pplan = a.pplan;
-				m.chunks = P->d_chunks.as<uint2>();
-				m.srec = P->d_srec.as<uint32_t>();
-				m.cmap = P->d_cmap.as<uint32_t>();
-				HIPCHK(ctx, launch_member_gather(m, P->n_chunks, a.rec, st));
-			}
 		} else {
 			// fresh R indexes (~0 = empty slot), then build + scan
 			a.ctab = P->d_ctab.as<uint32_t>();
@@ -832,7 +828,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	s.out_cap = out_cap;
 	s.status = d_status;
 	s.n_pairs = P->n;
-	if (P->ser_block) {
+	if (P->ser_block && !P->members) {   // (member mode: records are not gathered)
 		// A/B (DG_SER_BLOCK=1): block-per-pair serialiser, CRCs written in place
 		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
@@ -843,7 +839,26 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// 4. serialise everything but the header CRCs (the CRC stream may still
 	//    be running), then join and patch them in
 	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
-	HIPCHK(ctx, launch_serialize_wave(s, st));
+	if (P->members) {   // the chains' segment lists, one wave per chunk
+		MemSerArgs m{};
+		m.ver = d_ver;
+		m.pairs = s.pairs;
+		m.pplan = s.pplan;
+		m.chunks = P->d_chunks.as<uint2>();
+		m.cmap = P->d_cmap.as<uint32_t>();
+		m.seg = P->d_seg.as<uint32_t>();
+		m.nseg = P->d_nseg.as<uint32_t>();
+		m.mem_s = P->d_mem_s.as<uint32_t>();
+		m.srec = P->d_srec.as<uint32_t>();
+		m.rec = s.rec;
+		m.offsets = d_offsets;
+		m.out = d_out;
+		m.out_cap = out_cap;
+		m.status = d_status;
+		HIPCHK(ctx, launch_member_serialize(m, P->n_chunks, ctx->n_cu, st));
+	} else {
+		HIPCHK(ctx, launch_serialize_wave(s, st));
+	}
 	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
 	HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
 	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));

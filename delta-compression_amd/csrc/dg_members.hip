@@ -45,6 +45,7 @@
 
 #include "dg_device.h"
 #include "dg_devutil.h"
+#include "dg_serialize_wave.h"
 
 namespace dg {
 
@@ -485,7 +486,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 	if (lane == 0) {
 		a.csum[2ull * (pp.chunk_base + c)] = vp;
 		a.csum[2ull * (pp.chunk_base + c) + 1] = vbytes;
-		*(uint4*)(a.cmap + 4ull * (pp.chunk_base + c)) = make_uint4(0u, 0u, 0u, 0u);
+		*(uint2*)(a.cmap + 2ull * (pp.chunk_base + c)) = make_uint2(0u, 0u);   // no bulk piece yet
 	}
 }
 
@@ -512,20 +513,199 @@ __global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a, uint32_t n
 	}
 }
 
-// Copies every chunk's taken member records (the chain kernel's map: record
-// index, first and end member) into the pair's record array as (x, x, len,
-// ADD head) onepass records.
-__global__ __launch_bounds__(64) void member_gather_kernel(SpecArgs a, uint32_t* rec) {
+// ── member-mode serialisation ──────────────────────────────────────────
+
+// big-endian u32 / u8 at any byte address (unaligned LDS or global stores)
+template <typename P>
+__device__ __forceinline__ void put_be32(P p, uint32_t x) {
+	const uint32_t b = __builtin_bswap32(x);
+	__builtin_memcpy(p, &b, 4);
+}
+
+// Commands of up to 64 bulk members (lane = member) into dst at byte `my`
+// (LDS stage or, for an oversized tile, the output itself): ADD header and
+// payload, then the COPY.  Payloads come from the chunk's V bytes staged in
+// LDS (vb = position g0); a payload of > 64 bytes is copied by the whole wave.
+template <typename P>
+__device__ __forceinline__ void put_bulk(P dst, bool valid, uint32_t my, uint32_t prev, uint32_t x, uint32_t len,
+                                         uint32_t pw, const uint8_t* vb, int64_t g0) {
 	const uint32_t lane = lane_id();
-	const uint2 job = a.chunks[blockIdx.x];
-	const uint32_t pair = job.x, c = job.y;
-	const PairPlanDev pp = a.pplan[pair];
-	const uint4 m = *(const uint4*)(a.cmap + 4ull * (pp.chunk_base + c));   // (dst, from, to, -)
-	const uint64_t slot0 = pp.mem_base + (uint64_t)c * kMemChunkSlots;
-	uint32_t* out = rec + (uint64_t)kRecWordsOnepass * (pp.rec_base + m.x);
-	for (uint32_t i = m.y + lane; i < m.z; i += 64) {
-		const uint4 r = *(const uint4*)(a.srec + 4ull * (slot0 + i));
-		*(uint4*)(out + (uint64_t)kRecWordsOnepass * (i - m.y)) = make_uint4(r.x, r.x, r.y, r.z);
+	const uint32_t gap = x - prev;
+	const bool add = valid && gap != 0;
+	if (add) {
+		P q = dst + my;
+		q[0] = 2;
+		put_be32(q + 1, prev);
+		put_be32(q + 5, gap);
+		if (gap <= 4) {
+			__builtin_memcpy(q + 9, &pw, 4);   // spill past the payload lands in the COPY, written below
+		} else if (gap < 16) {
+			const uint8_t* src = vb + (prev - g0);
+			for (uint32_t k = 0; k < gap; k += 4) {   // spill <= 3 bytes: as above
+				uint32_t w;
+				__builtin_memcpy(&w, src + k, 4);
+				__builtin_memcpy(q + 9 + k, &w, 4);
+			}
+		} else if (gap <= 64) {
+			// 16-byte pieces, the last one ending at the payload's end (no spill)
+			const uint8_t* src = vb + (prev - g0);
+			for (uint32_t k = 0; k < gap; k += 16) {
+				const uint32_t kk = umin32(k, gap - 16);
+				uint4 w;
+				__builtin_memcpy(&w, src + kk, 16);
+				__builtin_memcpy(q + 9 + kk, &w, 16);
+			}
+		}
+	}
+	for (uint64_t bm = __ballot(add && gap > 64); bm; bm &= bm - 1) {
+		const uint32_t k = ffs64(bm);
+		const uint32_t src = rdlane(prev, k) - (uint32_t)g0, n = rdlane(gap, k), o = rdlane(my, k) + 9;
+		for (uint32_t i = 16 * lane; i < n; i += 1024) {
+			const uint32_t ii = umin32(i, n - 16);   // the last piece ends at the payload's end
+			uint4 w;
+			__builtin_memcpy(&w, vb + src + ii, 16);
+			__builtin_memcpy(dst + o + ii, &w, 16);
+		}
+	}
+	__builtin_amdgcn_wave_barrier();
+	if (valid) {
+		P q = dst + my + (gap ? 9u + gap : 0u);
+		q[0] = 1;
+		put_be32(q + 1, x);
+		put_be32(q + 5, x);
+		put_be32(q + 9, len);
+	}
+}
+
+constexpr uint32_t kMemSerStage = 4096;
+constexpr uint32_t kSerWavesPerCu = 16;
+
+// one job's inputs, loaded a job ahead (descriptors wave-uniform)
+struct SerFetch {
+	uint32_t pair, c, cnt, boff, first, vl;
+	int32_t st;
+	uint64_t base, end, slot0;
+	const uint8_t* V;
+	uint4 v[kStageRows];   // the chunk's staged V bytes (as the member kernel's)
+	uint4 r;               // member record of this lane (first 64)
+};
+
+__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, uint32_t j, SerFetch& F) {
+	const uint32_t lane = lane_id();
+	const uint2 jb = a.chunks[j];
+	F.pair = jb.x;
+	F.c = jb.y;
+	const PairDev pd = a.pairs[F.pair];
+	const PairPlanDev pp = a.pplan[F.pair];
+	F.vl = (uint32_t)pd.v_len;
+	F.V = a.ver + pd.v_off;
+	F.st = a.status[F.pair];
+	F.base = a.offsets[F.pair];
+	F.end = a.offsets[F.pair + 1];
+	const uint2 cm = *(const uint2*)(a.cmap + 2ull * (pp.chunk_base + F.c));
+	F.cnt = cm.x;
+	F.boff = cm.y;
+	F.slot0 = pp.mem_base + (uint64_t)F.c * kMemChunkSlots;
+	F.first = 0;
+	F.r = make_uint4(0u, 0u, 0u, 0u);
+	if (F.cnt && F.st == 0) {
+		const int64_t g0 = (int64_t)F.c * kMemChunk - 16;
+#pragma unroll
+		for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_tail(F.V, g0 + 1024 * k + 16 * lane, F.vl);
+		if (lane < F.cnt) F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));
+		F.first = a.mem_s[F.slot0];
+	}
+}
+
+// Member-mode serialisation: each chunk's job writes its bulk piece (the
+// members the chain took as they are, from the member records, payloads from
+// the chunk's V bytes in LDS) at the piece's byte offset, plus the pair's
+// segments 2c, 2c + 1 (record runs of the chain's own epochs, the tail), so
+// all the chunks of a pair serialise at once.  Persistent waves over
+// contiguous jobs, each job's inputs loaded while the previous one is written.
+__global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint32_t n_jobs) {
+	__shared__ __attribute__((aligned(16))) uint8_t vbuf[kStage + 16];
+	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
+	const uint32_t lane = lane_id();
+	const uint32_t j0 = (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
+	const uint32_t j1 = (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
+	SerFetch F, N;
+	if (j0 < j1) ser_fetch(a, j0, F);
+	for (uint32_t j = j0; j < j1; ++j) {
+		if (j + 1 < j1) ser_fetch(a, j + 1, N);
+		if (F.st == 0) {
+			if (F.end > a.out_cap) {
+				if (F.c == 0 && lane == 0) a.status[F.pair] = 7;
+			} else {
+				uint8_t* out = a.out + F.base;
+				if (F.c == 0) put_header(out, F.vl);
+				if (F.cnt) {
+					const int64_t g0 = (int64_t)F.c * kMemChunk - 16;
+					lds_order();
+#pragma unroll
+					for (uint32_t k = 0; k < kStageRows; ++k) *(uint4*)(vbuf + 1024 * k + 16 * lane) = F.v[k];
+					lds_order();
+					const uint8_t* vb = vbuf;
+					uint64_t pos = F.boff;
+					uint32_t prev_end = F.first;
+					for (uint32_t t0 = 0; t0 < F.cnt; t0 += 64) {
+						uint4 r = F.r;
+						if (t0 && t0 + lane < F.cnt) r = *(const uint4*)(a.srec + 4ull * (F.slot0 + t0 + lane));
+						const bool valid = t0 + lane < F.cnt;
+						const uint32_t x = r.x, len = r.y;
+						const uint32_t last = valid ? x + len : 0u;
+						uint32_t prev = wave_shr1(last);
+						if (lane == 0) prev = prev_end;
+						const uint32_t gap = x - prev;
+						const uint32_t sz = valid ? 13u + (gap ? 9u + gap : 0u) : 0u;
+						const uint32_t incl = wave_incl_scan(sz);
+						const uint32_t my = incl - sz;
+						const uint32_t S = rdlane(incl, 63);
+						if (S <= kMemSerStage) {
+							lds_order();
+							put_bulk(stage, valid, my, prev, x, len, r.z, vb, g0);
+							lds_order();
+							// flush: head bytes to a 16-byte boundary, 16-byte stores, tail bytes
+							uint8_t* dst = out + pos;
+							const uint32_t head = umin32((uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u), S);
+							if (lane < head) dst[lane] = stage[lane];
+							const uint32_t nq = (S - head) / 16;
+							uint4* dq = reinterpret_cast<uint4*>(dst + head);
+							for (uint32_t k = lane; k < nq; k += 64) {
+								uint4 w;
+								__builtin_memcpy(&w, stage + head + 16 * k, 16);
+								dq[k] = w;
+							}
+							const uint32_t tail0 = head + 16 * nq;
+							if (lane < S - tail0) dst[tail0 + lane] = stage[tail0 + lane];
+						} else {
+							put_bulk(out + pos, valid, my, prev, x, len, r.z, vb, g0);
+						}
+						pos += S;
+						const uint64_t has = __ballot(valid);
+						prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
+					}
+				}
+				// the chain's own record runs and the tail (segments 2c, 2c + 1;
+				// the pair's last chunk takes the rest)
+				const PairPlanDev& pp = a.pplan[F.pair];
+				const uint32_t ns = a.nseg[F.pair];
+				const uint32_t* seg = a.seg + 4ull * ((uint64_t)pp.chunk_base + 2ull * F.pair);
+				const uint32_t k1 = F.c + 1 == pp.n_chunks ? ns : umin32(2 * F.c + 2, ns);
+				for (uint32_t k = 2 * F.c; k < k1; ++k) {
+					const uint4 e = *(const uint4*)(seg + 4ull * k);
+					uint8_t* o = out + e.z;
+					if (e.x == kSegTail) {
+						const uint64_t n = put_tail(o, F.V, F.vl, e.w);
+						if (e.z + n != F.end - F.base && lane == 0) a.status[F.pair] = 5;   // sizes disagree
+					} else {
+						const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (pp.rec_base + e.x), kRecWordsOnepass};
+						serialize_run<kMemSerStage, 1>(o, F.V, F.vl, src, e.y, e.w, (sw_lds8*)stage);
+					}
+				}
+			}
+		}
+		F = N;
 	}
 }
 
@@ -536,9 +716,10 @@ hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, h
 	return hipGetLastError();
 }
 
-hipError_t launch_member_gather(const SpecArgs& a, uint32_t n_chunks, uint32_t* rec, hipStream_t st) {
+hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {
 	if (n_chunks == 0) return hipSuccess;
-	hipLaunchKernelGGL(member_gather_kernel, dim3(n_chunks), dim3(64), 0, st, a, rec);
+	const uint32_t waves = std::min<uint32_t>(n_chunks, kSerWavesPerCu * std::max(n_cu, 1u));
+	hipLaunchKernelGGL(member_serialize_kernel, dim3(waves), dim3(64), 0, st, a, n_chunks);
 	return hipGetLastError();
 }
 

@@ -723,7 +723,33 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	const uint32_t* ncp = nullptr;   // members per chunk
 	bool mem_live = false;           // members remain ahead of the chain
 	const uint32_t* csp = nullptr;   // per chunk: verified prefix, its delta bytes
-	uint32_t* cmp = nullptr;         // per chunk: bulk range -> record index (member_gather_kernel)
+	uint32_t* cmp = nullptr;         // per chunk: bulk piece (member count, byte offset)
+	// the delta's other pieces (member_serialize_kernel): the runs of records
+	// this chain wrote itself (between bulk pieces, so at most n_chunks + 1)
+	// and the tail
+	uint32_t* sgp = nullptr;
+	uint32_t nseg = 0, seg_cap = 0;
+	bool nb_open = false;            // a run of records written here is open
+	uint32_t nb_first = 0, nb_boff = 0, nb_prev = 0;
+	auto nb_note = [&]() {           // before records are appended to rec
+		if (!nb_open) {
+			nb_open = true;
+			nb_first = nrec;
+			nb_boff = (uint32_t)(dsz - 1);   // dsz counts the END byte
+			nb_prev = v0;
+		}
+	};
+	auto nb_close = [&]() {
+		if (nb_open && nrec > nb_first) {
+			if (nseg < seg_cap) {
+				if (lane == 0) *(uint4*)(sgp + 4ull * nseg) = make_uint4(nb_first, nrec - nb_first, nb_boff, nb_prev);
+			} else {
+				st = 5;
+			}
+			++nseg;
+		}
+		nb_open = false;
+	};
 	auto take_members = [&]() {
 		[[maybe_unused]] const uint64_t tt0 = PROF_NOW();
 		if constexpr (Src::kPhaseA) PROF_ADD(src, P_TAKES, 1);
@@ -745,8 +771,12 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				const uint32_t incl = wave_incl_scan(ct);
 				const uint32_t tot = rdlane(incl, 63);
 				if (nrec + tot > rec_cap) { st = 7; scanning = false; return; }
-				if (use) *(uint4*)(cmp + 4ull * cj) = make_uint4(nrec + incl - ct, 0u, ct, 0u);
-				dsz += rdlane(wave_incl_scan(use ? vb : 0u), 63);
+				nb_close();
+				// the chunks' bulk pieces: member count and byte offset
+				const uint32_t bvb = use ? vb : 0u;
+				const uint32_t bi = wave_incl_scan(bvb);
+				if (use && ct > 0) *(uint2*)(cmp + 2ull * cj) = make_uint2(ct, (uint32_t)(dsz - 1) + bi - bvb);
+				dsz += rdlane(bi, 63);
 				nrec += tot;
 				if (nfull == 64) { kc += 64; continue; }
 				kc += nfull;
@@ -768,6 +798,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			const uint64_t bad = ~__ballot(lane < n_in && r4.w != 0u) & full;
 			const uint32_t take = bad ? ffs64(bad) : n_in;   // the verified prefix
 			if (nrec + take > rec_cap) { st = 7; scanning = false; return; }
+			if (take) nb_note();
 			if (lane < take) *(uint4*)(rec + (uint64_t)kRecWordsOnepass * (nrec + lane)) = make_uint4(r4.x, r4.x, r4.y, r4.z);
 			const uint32_t gap = r4.x - sj;   // ADD [s_j, x_j) before the COPY
 			const uint32_t sz = lane < take ? 13u + (gap ? 9u + gap : 0u) : 0u;
@@ -786,12 +817,16 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		at_mismatch = kc != 0 || ki != 0;   // member starts past the first are mismatches
 		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_TAKE, PROF_NOW() - tt0);
 	};
+	if (members) {
+		sgp = a.seg + 4ull * ((uint64_t)pp.chunk_base + 2ull * pair);
+		seg_cap = uni(pp.n_chunks) + 2;
+	}
 	if (members && scanning) {
 		msp = a.mem_s + pp.mem_base;
 		srp = a.srec + 4ull * pp.mem_base;
 		ncp = a.n_mem + pp.chunk_base;
 		csp = a.csum + 2ull * pp.chunk_base;
-		cmp = a.cmap + 4ull * pp.chunk_base;
+		cmp = a.cmap + 2ull * pp.chunk_base;
 		nch = uni(pp.n_chunks);
 		cnt = uni(ncp[0]);
 		take_members();
@@ -832,6 +867,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		if constexpr (Src::kPhaseA) {
 			if (at_mismatch) {
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
+				if (members) nb_note();
 				const auto dg = src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm);
 				const uint32_t f = uni(dg.committed);
 				skipA = f == 0 && uni(dg.long_first) != 0u;
@@ -1078,6 +1114,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				pw = w;
 			}
 		}
+		if (members) nb_note();
 		if (lane < 4) rec[kRecWordsOnepass * nrec + lane] = lane == 0 ? vm : (lane == 1 ? rm : (lane == 2 ? ml : pw));
 		++nrec;
 		dsz += 13 + (vm > v0 ? 9 + (uint64_t)(vm - v0) : 0);
@@ -1085,7 +1122,18 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		r0 = rm + ml;
 		at_mismatch = true;
 	}
+	if (members && st == 0) {
+		nb_close();
+		if (nseg < seg_cap) {
+			if (lane == 0) *(uint4*)(sgp + 4ull * nseg) = make_uint4(kSegTail, 0u, (uint32_t)(dsz - 1), v0);
+		} else {
+			st = 5;
+		}
+		++nseg;
+		if (lane == 0) a.nseg[pair] = nseg;
+	}
 	if (v0 < vl) dsz += 9 + (uint64_t)(vl - v0);   // trailing ADD (:268-275)
+	if (members && (dsz >> 32)) st = 7;   // segment offsets are 32-bit
 
 	if (tslot >= 0) release_table();
 	if (lane == 0) {

@@ -155,24 +155,30 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 		}
 }
 
-// Wave-wide serialisation of one pair.  `out` = the pair's first output
-// byte, `size` = its delta size (as accumulated by the differencing), `rec`
-// its COPY records (v, r, len) in V order, `stage` >= kStageBytes of LDS.
-// kCmd records per lane per tile (64 * kCmd commands per tile: fewer
-// dependent load rounds per pair).  Returns 0, or 5 when the bytes written
-// disagree with `size`.
-template <uint32_t kStageBytes, int kCmd = 1>
-__device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint8_t* V, uint32_t vl,
-                                         const uint32_t* rec, uint32_t W, uint32_t n, sw_lds8* stage) {
-	const bool inl = W >= 4;   // 4th record word: V bytes from the gap start
-	const uint32_t lane = lane_id();
-	if (lane == 0) {
-		out[0] = 'D'; out[1] = 'L'; out[2] = 'T'; out[3] = 3;
-		out[4] = 0;   // standard delta
-		be32_store(out + 5, vl);
+// Record sources for serialize_run: COPY record j as (v, r, len, ADD head).
+struct RecWords {   // the record arrays: W words per record, ADD head in the 4th when W >= 4
+	const uint32_t* rec;
+	uint32_t W;
+	static constexpr bool kAlwaysHead = false;
+	__device__ bool inl() const { return W >= 4; }
+	__device__ void load(uint32_t j, uint32_t& v, uint32_t& r, uint32_t& l, uint32_t& w) const {
+		v = rec[W * j];
+		r = rec[W * j + 1];
+		l = rec[W * j + 2];
+		w = W >= 4 ? rec[W * j + 3] : 0u;
 	}
-	uint64_t pos = 25;
-	uint32_t prev_end = 0;   // end of the previous tile's last COPY
+};
+
+// Serialises n consecutive COPY records (each preceded by the ADD of its gap)
+// from `out`; prev_end = the V position the first gap starts at.  kCmd
+// records per lane per tile (64 * kCmd commands per tile: fewer dependent
+// load rounds).  Returns the bytes written.
+template <uint32_t kStageBytes, int kCmd, class Src>
+__device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_t vl, const Src& src, uint32_t n,
+                                         uint32_t prev_end, sw_lds8* stage) {
+	const bool inl = src.inl();
+	const uint32_t lane = lane_id();
+	uint64_t pos = 0;
 	// the next tile's records are loaded while this tile is assembled: their
 	// latency hides under this tile's payload loads
 	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd], ncw[kCmd];
@@ -180,12 +186,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 	for (int i = 0; i < kCmd; ++i) {
 		const uint32_t j = kCmd * lane + i;
 		ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
-		if (j < n) {
-			ncv[i] = rec[W * j];
-			ncr[i] = rec[W * j + 1];
-			ncl[i] = rec[W * j + 2];
-			if (inl) ncw[i] = rec[W * j + 3];
-		}
+		if (j < n) src.load(j, ncv[i], ncr[i], ncl[i], ncw[i]);
 	}
 	for (uint32_t t0 = 0; t0 < n; t0 += 64 * kCmd) {
 		bool valid[kCmd];
@@ -200,12 +201,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			cw[i] = ncw[i];
 			const uint32_t jn = j + 64 * kCmd;
 			ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
-			if (jn < n) {
-				ncv[i] = rec[W * jn];
-				ncr[i] = rec[W * jn + 1];
-				ncl[i] = rec[W * jn + 2];
-				if (inl) ncw[i] = rec[W * jn + 3];
-			}
+			if (jn < n) src.load(jn, ncv[i], ncr[i], ncl[i], ncw[i]);
 		}
 		// the lane's last valid command end, and the lane's byte count
 		uint32_t last = 0, sz = 0;
@@ -224,14 +220,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 					pv = cv[i] + cl[i];
 				}
 		}
-		// inclusive prefix of the sizes (DPP network; tile bytes < 4 GiB)
-		uint32_t incl = sz;
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, false);
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xF, 0xF, false);
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xF, 0xF, false);
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xF, 0xF, false);
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x142, 0xA, 0xF, false);
-		incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x143, 0xC, 0xF, false);
+		const uint32_t incl = wave_incl_scan(sz);   // tile bytes < 4 GiB
 		const uint32_t my = incl - sz;
 		const uint32_t S = rdlane(incl, 63);
 		if (S <= kStageBytes) {
@@ -260,24 +249,61 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, cw, inl, V, vl);
 		}
 		pos += S;
-		prev_end = rdlane(last, 63);
 		{   // lanes past the end hold last = 0: take the highest lane with a command
 			const uint64_t has = __ballot(valid[0]);
 			if (has) prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
 		}
 	}
-	if (prev_end < vl) {   // trailing ADD (src/c/onepass.c:268-275)
-		const uint32_t len = vl - prev_end;
+	return pos;
+}
+
+// The delta header without its CRCs (bytes 9..24, crc_patch_kernel), lane 0
+__device__ __forceinline__ void put_header(uint8_t* out, uint32_t vl) {
+	if (lane_id() == 0) {
+		out[0] = 'D'; out[1] = 'L'; out[2] = 'T'; out[3] = 3;
+		out[4] = 0;   // standard delta
+		be32_store(out + 5, vl);
+	}
+}
+
+// The trailing ADD of V[from, vl) (src/c/onepass.c:268-275) and END; returns
+// the bytes written.
+__device__ __forceinline__ uint64_t put_tail(uint8_t* out, const uint8_t* V, uint32_t vl, uint32_t from) {
+	const uint32_t lane = lane_id();
+	uint64_t pos = 0;
+	if (from < vl) {
+		const uint32_t len = vl - from;
 		if (lane == 0) {
-			out[pos] = 2;
-			be32_store(out + pos + 1, prev_end);
-			be32_store(out + pos + 5, len);
+			out[0] = 2;
+			be32_store(out + 1, from);
+			be32_store(out + 5, len);
 		}
-		for (uint32_t i = lane; i < len; i += 64) out[pos + 9 + i] = V[prev_end + i];
-		pos += 9 + len;
+		for (uint32_t i = lane; i < len; i += 64) out[9 + i] = V[from + i];
+		pos = 9 + len;
 	}
 	if (lane == 0) out[pos] = 0;   // END
-	return pos + 1 == size ? 0 : 5;
+	return pos + 1;
+}
+
+// Wave-wide serialisation of one pair.  `out` = the pair's first output
+// byte, `size` = its delta size (as accumulated by the differencing), `rec`
+// its COPY records (v, r, len) in V order, `stage` >= kStageBytes of LDS.
+// Returns 0, or 5 when the bytes written disagree with `size`.
+template <uint32_t kStageBytes, int kCmd = 1>
+__device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint8_t* V, uint32_t vl,
+                                         const uint32_t* rec, uint32_t W, uint32_t n, sw_lds8* stage) {
+	put_header(out, vl);
+	uint64_t pos = 25;
+	const RecWords src{rec, W};
+	pos += serialize_run<kStageBytes, kCmd>(out + pos, V, vl, src, n, 0u, stage);
+	// the end of the last COPY
+	uint32_t prev_end = 0;
+	if (n) {
+		const uint32_t* r = rec + (uint64_t)W * (n - 1);
+		prev_end = r[0] + r[2];
+	}
+	pos += put_tail(out + pos, V, vl, prev_end);
+	return pos == size ? 0 : 5;
 }
 
 }  // namespace dg
