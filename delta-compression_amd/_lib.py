@@ -149,7 +149,12 @@ def _load() -> C.CDLL:
                                                       C.POINTER(u64), C.POINTER(u64), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if os.environ.get("DG_LIB_VARIANT"):   # an older A/B baseline build
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     return L
@@ -253,7 +258,8 @@ class EncodePlan:
     @property
     def members(self) -> bool:
         """True when onepass runs through verified diagonal members."""
-        return bool(lib.dg_encode_plan_flags(self.handle) & 1)
+        fn = getattr(lib, "dg_encode_plan_flags", None)   # (absent from older A/B baselines)
+        return bool(fn(self.handle) & 1) if fn else False
 
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)

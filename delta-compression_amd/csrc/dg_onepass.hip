@@ -676,7 +676,7 @@ struct PairResult {
 	int32_t st;
 };
 
-template <class Src>
+template <bool kMembers, class Src>
 __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
                                              uint32_t* bm) {
@@ -716,7 +716,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	//    run only from an unverified member until the chain lands on a later
 	//    member start, and for the final epoch (whose member is never
 	//    verified: its run holds the end of the shorter stream) ──
-	const bool members = Src::kPhaseA && a.srec != nullptr;
+	constexpr bool members = kMembers && Src::kPhaseA;   // (the plain chain compiles none of it)
 	uint32_t kc = 0, ki = 0, nch = 0, cnt = 0, s_cur = 0;   // chunk, index in chunk, chunks, members in kc
 	const uint32_t* msp = nullptr;   // member starts of chunk 0 (chunk c: + c * kMemChunkSlots)
 	const uint32_t* srp = nullptr;
@@ -1102,7 +1102,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			}
 		}
 		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_BC, PROF_NOW() - tb);
-		if (in_table) release_table();   // held for this epoch only: the pool serves the other waves
+		if (members && in_table) release_table();   // member mode: held for this epoch only
 		if (!matched) break;
 
 		// emit ADD (implicit gap) + COPY, flush the tables (:243-263)
@@ -1155,7 +1155,10 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	return PairResult{nrec, dsz, st};
 }
 
-// p = 16, 16-byte aligned pairs: LDS windows (the hot configuration)
+// p = 16, 16-byte aligned pairs: LDS windows (the hot configuration); the
+// member-mode chain is its own instance so the plain chain carries none of
+// its registers
+template <bool kMembers>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
@@ -1181,7 +1184,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
-	const PairResult res = onepass_pair(src, a, pair, pd, pp, 16u, bm);
+	const PairResult res = onepass_pair<kMembers>(src, a, pair, pd, pp, 16u, bm);
 #ifdef DG_REFILL_PROF
 	if (lane_id() == 0) {
 		atomicAdd(&g_refill_prof[0], (unsigned long long)src.refill_cycles);
@@ -1190,7 +1193,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	}
 #endif
 	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
-	if (a.lookback) {
+	if (!kMembers && a.lookback) {
 		// fused placement + serialisation (dg_serialize_wave.h)
 		const uint64_t off = lookback_offset(a.lookback, pair, res.dsz);
 		const uint32_t lane = lane_id();
@@ -1224,7 +1227,7 @@ __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	GlobalSrc<PF> src{a.ver + pd.v_off, a.ref + pd.r_off, PF > 0 ? (uint32_t)PF : a.p, a.powc};
-	onepass_pair(src, a, pair, pd, pp, src.p, bm);
+	onepass_pair<false>(src, a, pair, pd, pp, src.p, bm);
 }
 
 // DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B builds only)
@@ -1238,7 +1241,10 @@ bool onepass16_selected() { return !force_global_src(); }
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
 	if (a.n_pairs == 0) return hipSuccess;
 	if (p == 16 && aligned16 && !force_global_src())
-		hipLaunchKernelGGL(onepass16_kernel, dim3(a.n_pairs), dim3(64), 0, st, a);
+		if (a.srec)
+			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(a.n_pairs), dim3(64), 0, st, a);
+		else
+			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), 0, st, a);
 	else if (a.lookback)
 		return hipErrorInvalidValue;   // fused serialisation needs onepass16_kernel
 	else if (p == 16)
