@@ -115,7 +115,7 @@ constexpr uint32_t kSegTail = 0xFFFFFFFFu;
 // staged for the members that end past the chunk.  Members start >= p = 16
 // bytes apart, so a chunk holds at most kMemChunk / 16 of them.
 constexpr uint32_t kMemChunk = 2048;
-constexpr uint32_t kMemAhead = 1008;   // staged: [chunk - 16, chunk + 2048 + 1008) = 3 KiB
+constexpr uint32_t kMemAhead = 240;    // staged: [chunk - 16, chunk + 2048 + 240) = 2304 B
 constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
 
 struct SpecArgs {

@@ -55,7 +55,10 @@ constexpr uint32_t kStage = kMemChunk + kMemAhead + 16;   // staged bytes per st
 constexpr uint32_t kMaskWords = (kStage + 31) / 32;        // mismatch bitmap words
 constexpr uint32_t kRunList = kStage / 17 + 4;             // run starts in the staged region (>= 17 apart)
 constexpr uint32_t kLongChunks = 8;
-constexpr uint32_t kMemWavesPerCu = 16;                    // persistent waves (LDS allows 17)                        // members of up to 512 steps are verified
+constexpr uint32_t kMemWavesPerCu = 16;
+#ifndef DG_MEM_WAVES
+#define DG_MEM_WAVES 7   // minimum waves per SIMD the register budget must allow
+#endif                    // persistent waves (LDS allows 17)                        // members of up to 512 steps are verified
 static_assert(kStage % 16 == 0, "16-byte blocks");
 
 // 16 mismatch bits of 16 bytes (bit i: byte i of the chunk differs)
@@ -105,12 +108,10 @@ struct ChunkLds {
 	uint8_t v[kStage + 16];   // + slack: the fifth dword of a window read
 	uint8_t r[kStage + 16];
 	uint32_t mask[kMaskWords];
-	uint32_t last[kMaskWords];   // max mismatch offset + 1 over words <= j (0: none)
+	uint16_t last[kMaskWords];   // max mismatch offset + 1 over words <= j (0: none)
 	uint16_t run[kRunList];      // run starts (offsets), ascending
-	uint32_t mark[64];
-	uint32_t filt[256];          // V-hash filter: short rounds 64 words, long members 64 / 256
-	uint8_t ok[kMemChunkSlots];  // per member of the chunk: verified
-	uint16_t sz[kMemChunkSlots]; // per member: its ADD + COPY bytes in the delta
+	uint8_t mark[64];
+	uint32_t filt[64];           // V-hash filter of a round or a long member
 };
 
 // the 16 bytes at offset o of a staged stream: one unaligned ds_read_b128
@@ -223,47 +224,110 @@ __device__ __forceinline__ bool long_member_ok(const uint8_t* SV, const uint8_t*
 
 // the staged region of one chunk in VGPRs (16 bytes per lane per row), loaded
 // while the previous chunk is verified
-constexpr uint32_t kStageRows = kStage / 1024;
-static_assert(kStage % 1024 == 0, "whole rows");
+constexpr uint32_t kStageRows = (kStage + 1023) / 1024;   // rows of 64 x 16 B (the last one partial)
 struct StageRegs {
 	uint4 v[kStageRows], r[kStageRows];
 };
 
-// 16 bytes of a stream at p (16-aligned; bytes at or past len read as 0)
-__device__ __forceinline__ uint4 load16_tail(const uint8_t* S, int64_t p, uint32_t len) {
-	if (p < 0 || p >= (int64_t)len) return make_uint4(0u, 0u, 0u, 0u);
-	if (p + 16 <= (int64_t)len) return *(const uint4*)(S + p);
+// A wave's walk over its contiguous run of (pair, chunk) jobs: the jobs are
+// laid out pair after pair, chunk after chunk, so the next job follows from
+// this one and only a new pair's descriptors are loaded (wave-uniform).
+struct JobCursor {
+	uint32_t pair, c, n_chunks, chunk_base;
+	uint32_t vl, rl;
+	uint64_t v_off, r_off, mem_base, q, q_magic, rec_base;
+	template <class Args>
+	__device__ void load_pair(const Args& a) {
+		const PairDev& pd = a.pairs[pair];
+		const PairPlanDev& pp = a.pplan[pair];
+		v_off = pd.v_off;
+		r_off = pd.r_off;
+		vl = (uint32_t)pd.v_len;
+		rl = (uint32_t)pd.r_len;
+		mem_base = pp.mem_base;
+		q = pp.q;
+		q_magic = pp.q_magic;
+		chunk_base = pp.chunk_base;
+		n_chunks = pp.n_chunks;
+		rec_base = pp.rec_base;
+	}
+	template <class Args>
+	__device__ void start(const Args& a, uint32_t job) {
+		const uint2 jb = a.chunks[job];
+		pair = uni(jb.x);
+		c = uni(jb.y);
+		load_pair(a);
+	}
+	template <class Args>
+	__device__ void next(const Args& a) {
+		if (c + 1 < n_chunks) {
+			++c;
+		} else {
+			++pair;
+			c = 0;
+			load_pair(a);
+		}
+	}
+};
+
+__device__ const uint4 g_zero16 = {0u, 0u, 0u, 0u};
+
+// 16 bytes of a stream at p (16-aligned), issued without a wait: a piece
+// wholly inside the stream loads directly, any other reads a zero block; the
+// one piece per stream that straddles its end is rebuilt from bytes at use
+// (stage_piece), so no load sits in a branch the compiler must drain.
+__device__ __forceinline__ uint4 load16_async(const uint8_t* S, int64_t p, uint32_t len) {
+	const bool full = p >= 0 && p + 16 <= (int64_t)len;
+	return *(const uint4*)(full ? S + p : (const uint8_t*)&g_zero16);
+}
+
+__device__ __forceinline__ uint4 stage_piece(const uint4& v, const uint8_t* S, int64_t p, uint32_t len) {
+	if (!(p >= 0 && p < (int64_t)len && p + 16 > (int64_t)len)) return v;
 	uint32_t w[4] = {0u, 0u, 0u, 0u};
 	for (uint32_t b = 0; p + b < (int64_t)len; ++b) w[b >> 2] |= (uint32_t)S[p + b] << (8 * (b & 3u));
 	return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__device__ __forceinline__ void stage_load(const SpecArgs& a, uint32_t job, StageRegs& S) {
-	const uint2 jb = a.chunks[job];
-	const PairDev pd = a.pairs[jb.x];
-	const int64_t g0 = (int64_t)jb.y * kMemChunk - 16;
-	const uint8_t* V = a.ver + pd.v_off;
-	const uint8_t* R = a.ref + pd.r_off;
+__device__ __forceinline__ void stage_load(const SpecArgs& a, const JobCursor& J, StageRegs& S) {
+	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
+	const uint8_t* V = a.ver + J.v_off;
+	const uint8_t* R = a.ref + J.r_off;
 	const uint32_t lane = lane_id();
 #pragma unroll
 	for (uint32_t k = 0; k < kStageRows; ++k) {
 		const int64_t p = g0 + 1024 * k + 16 * lane;
-		S.v[k] = load16_tail(V, p, (uint32_t)pd.v_len);
-		S.r[k] = load16_tail(R, p, (uint32_t)pd.r_len);
+		S.v[k] = load16_async(V, p, J.vl);
+		S.r[k] = load16_async(R, p, J.rl);
 	}
 }
 
-__device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uint32_t job) {
+// the staged bytes into LDS (straddling pieces rebuilt here)
+__device__ __forceinline__ void stage_store(const SpecArgs& a, const JobCursor& J, const StageRegs& S, ChunkLds& L) {
+	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
 	const uint32_t lane = lane_id();
-	const uint2 jb = a.chunks[job];   // (pair, chunk)
-	const uint32_t pair = jb.x, c = jb.y;
-	const PairDev pd = a.pairs[pair];
-	const PairPlanDev pp = a.pplan[pair];
-	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
+	const uint32_t vl = J.vl, rl = J.rl;
+	const bool tail = g0 + (int64_t)kStage > (int64_t)umin32(vl, rl);   // (uniform) the streams end in this region
+#pragma unroll
+	for (uint32_t k = 0; k < kStageRows; ++k) {
+		const int64_t p = g0 + 1024 * k + 16 * lane;
+		uint4 v = S.v[k], r = S.r[k];
+		if (tail) {
+			v = stage_piece(v, a.ver + J.v_off, p, vl);
+			r = stage_piece(r, a.ref + J.r_off, p, rl);
+		}
+		*(uint4*)(L.v + 1024 * k + 16 * lane) = v;
+		*(uint4*)(L.r + 1024 * k + 16 * lane) = r;
+	}
+}
+
+__device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, const JobCursor& J) {
+	const uint32_t lane = lane_id();
+	const uint32_t pair = J.pair, c = J.c;
+	const uint32_t vl = J.vl, rl = J.rl;
 	const uint32_t E = umin32(vl, rl);
 	const uint32_t cw = c * kMemChunk;                  // chunk start (position)
 	const int64_t g0 = (int64_t)cw - 16;                // position of staged offset 0
-	const uint64_t slot0 = pp.mem_base + (uint64_t)c * kMemChunkSlots;
+	const uint64_t slot0 = J.mem_base + (uint64_t)c * kMemChunkSlots;
 
 	// ── 2. mismatch bitmap: bit o = position g0 + o differs (or is E, the
 	//    sentinel); chunk 0's lookbehind holds only the virtual mismatch at -1 ──
@@ -300,7 +364,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 		if (j == 0) rs &= ~0xFFFFu;   // the lookbehind starts no run
 		const uint32_t last1 = m ? 32 * j + 32u - (uint32_t)__builtin_clz(m) : 0u;
 		const uint32_t lm = umax32(wave_incl_max(last1), carry);
-		if (in) L.last[j] = lm;
+		if (in) L.last[j] = (uint16_t)lm;
 		carry = rdlane(lm, 63);
 		const uint32_t cnt = (uint32_t)__builtin_popcount(rs);
 		const uint32_t incl = wave_incl_scan(cnt);
@@ -320,14 +384,16 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 		const uint32_t i = i0 + lane;
 		nm += (uint32_t)__builtin_popcountll(__ballot(i < nrun && L.run[i] < 16 + kMemChunk));
 	}
-	if (lane == 0) a.n_mem[pp.chunk_base + c] = nm;
+	if (lane == 0) a.n_mem[J.chunk_base + c] = nm;
 
-	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
+	const uint64_t q = J.q, qmag = J.q_magic;
 	const ModQ mq = make_modq(q, qmag);
 	VFilter<64> fs{L.filt};
 	const uint8_t* SV = L.v;
 	const uint8_t* SR = L.r;
 
+	uint32_t vp = 0, vbytes = 0;   // verified prefix of the chunk's members, its delta bytes
+	bool open = true;
 	for (uint32_t k0 = 0; k0 < nm; k0 += 64) {
 		// lane m: member k0 + m (offsets; x = last mismatch before the next
 		// run start + 1; a member whose next start is unknown stays unverified)
@@ -348,10 +414,9 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 		const uint32_t P = wave_incl_scan(shrt ? T + 1 : 0u);   // packed end of each short member
 		uint32_t* mem_s = a.mem_s + slot0 + k0;
 		uint32_t* srec = a.srec + 4ull * (slot0 + k0);
+		bool myok = false;   // this lane's member verified
 		if (mine) {
 			mem_s[lane] = (uint32_t)(g0 + (int64_t)s);
-			L.ok[i] = 0;
-			L.sz[i] = (uint16_t)(13u + (T ? 9u + T : 0u));
 			if (!known || T >= 64u * kLongChunks)   // unverified: the chain runs its epoch exactly
 				*(uint4*)(srec + 4 * lane) = make_uint4(0u, 0u, 0u, 0u);
 		}
@@ -373,7 +438,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 			fs.clear();
 			lds_order();
 			const uint32_t st = P - (T + 1) - done;   // first step lane (members in the round)
-			if (in) L.mark[st] = lane + 1u;
+			if (in) L.mark[st] = (uint8_t)(lane + 1u);
 			lds_order();
 			const bool live = lane < B;
 			const uint32_t mk = wave_incl_max(L.mark[lane]);   // lane 0 always holds a mark
@@ -443,7 +508,11 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 				const uint32_t xx = (uint32_t)(g0 + (int64_t)(ms_j + mt_j));
 				const uint32_t v = (BA & mem) == 0 ? 1u : 0u;
 				*(uint4*)(srec + 4 * mj) = make_uint4(xx, snj - (ms_j + mt_j), pw, v);
-				L.ok[k0 + mj] = (uint8_t)v;
+			}
+			{   // each member lane takes its verdict from its T step's lane
+				const uint32_t vT = isT && (BA & mem) == 0 ? 1u : 0u;
+				const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((P - done - 1u) << 2), (int)vT);
+				if (in) myok = got != 0u;
 			}
 			done += B;
 		}
@@ -457,60 +526,66 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, uin
 			const uint32_t M = ffs64(LM);
 			const uint32_t s0 = rdlane(s, M), tl = rdlane(T, M), sn0 = rdlane(sn, M);
 			uint32_t pw;
-			const bool ok = tl < 128 ? long_member_ok<64>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw)
-			                         : long_member_ok<256>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw);
+			const bool ok = long_member_ok<64>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw);
 			if (lane == 0) {
 				*(uint4*)(srec + 4 * M) = make_uint4((uint32_t)(g0 + (int64_t)(s0 + tl)), sn0 - (s0 + tl), pw,
 				                                     ok ? 1u : 0u);
-				L.ok[k0 + M] = ok ? 1u : 0u;
 			}
+			if (lane == M) myok = ok;
+		}
+		// the chunk's verified prefix through this batch
+		if (open) {
+			const uint32_t lim2 = k1 - k0;
+			const uint64_t live = lim2 == 64 ? ~0ull : ((1ull << lim2) - 1ull);
+			const uint64_t gaps = ~__ballot(mine && myok) & live;
+			const uint32_t take = gaps ? ffs64(gaps) : lim2;
+			const uint32_t b = lane < take ? 13u + (T ? 9u + T : 0u) : 0u;
+			vbytes += rdlane(wave_incl_scan(b), 63);
+			vp += take;
+			open = take == lim2;
 		}
 	}
 	// ── 5. chunk summary for the chain: the verified prefix and its delta
-	//    bytes; the gather map starts empty ──
-	lds_fence();
-	uint32_t vp = 0, vbytes = 0;
-	bool open = true;
-	for (uint32_t k0 = 0; k0 < nm && open; k0 += 64) {
-		const uint32_t i = k0 + lane;
-		const bool v = i < nm && L.ok[i];
-		const uint32_t lim2 = umin32(nm - k0, 64u);
-		const uint64_t live = lim2 == 64 ? ~0ull : ((1ull << lim2) - 1ull);
-		const uint64_t gaps = ~__ballot(v) & live;
-		const uint32_t take = gaps ? ffs64(gaps) : lim2;
-		const uint32_t b = lane < take ? (uint32_t)L.sz[i] : 0u;
-		vbytes += rdlane(wave_incl_scan(b), 63);
-		vp += take;
-		open = take == lim2;
-	}
+	//    bytes (accumulated per batch above) ──
 	if (lane == 0) {
-		a.csum[2ull * (pp.chunk_base + c)] = vp;
-		a.csum[2ull * (pp.chunk_base + c) + 1] = vbytes;
-		*(uint2*)(a.cmap + 2ull * (pp.chunk_base + c)) = make_uint2(0u, 0u);   // no bulk piece yet
+		a.csum[2ull * (J.chunk_base + c)] = vp;
+		a.csum[2ull * (J.chunk_base + c) + 1] = vbytes;
+		*(uint2*)(a.cmap + 2ull * (J.chunk_base + c)) = make_uint2(0u, 0u);   // no bulk piece yet
 	}
 }
 
-// Persistent waves over contiguous runs of chunks (the look-ahead a chunk
-// shares with the next one stays in this XCD's L2): the next chunk's bytes
-// are loaded into VGPRs while this one is verified, so no wave waits on HBM.
-__global__ __launch_bounds__(64) void member_chunk_kernel(SpecArgs a, uint32_t n_chunks) {
+// One wave per (pair, chunk) job.  The chunk's bytes are staged by LDS-DMA
+// (no VGPRs held for them), which keeps the wave within 96 VGPRs and 8 KiB
+// of LDS: 5 waves per SIMD to hide the LDS and DMA latencies of the rounds.
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_MEM_WAVES, 8))) void member_chunk_kernel(SpecArgs a, uint32_t n_chunks) {
 	__shared__ __attribute__((aligned(16))) ChunkLds L;
 	const uint32_t lane = lane_id();
-	const uint32_t j0 = (uint32_t)((uint64_t)n_chunks * blockIdx.x / gridDim.x);
-	const uint32_t j1 = (uint32_t)((uint64_t)n_chunks * (blockIdx.x + 1) / gridDim.x);
-	StageRegs S;
-	if (j0 < j1) stage_load(a, j0, S);
-	for (uint32_t j = j0; j < j1; ++j) {
-		lds_order();   // the previous chunk's LDS reads are issued
+	JobCursor J;
+	J.start(a, blockIdx.x);
+	{
+		const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
+		const uint8_t* V = a.ver + J.v_off;
+		const uint8_t* R = a.ref + J.r_off;
 #pragma unroll
 		for (uint32_t k = 0; k < kStageRows; ++k) {
-			*(uint4*)(L.v + 1024 * k + 16 * lane) = S.v[k];
-			*(uint4*)(L.r + 1024 * k + 16 * lane) = S.r[k];
+			const int64_t p = g0 + 1024 * k + 16 * lane;
+			if (1024 * k + 16 * lane >= kStage) continue;
+			// whole pieces by DMA; the piece straddling a stream's end (and
+			// the lookbehind before position 0) through registers
+			if (p >= 0 && p + 16 <= (int64_t)J.vl)
+				__builtin_amdgcn_global_load_lds((const void*)(V + p), (lds_void_t*)(L.v + 1024 * k), 16, 0, 0);
+			else
+				*(uint4*)(L.v + 1024 * k + 16 * lane) = stage_piece(make_uint4(0u, 0u, 0u, 0u), V, p, J.vl);
+			if (p >= 0 && p + 16 <= (int64_t)J.rl)
+				__builtin_amdgcn_global_load_lds((const void*)(R + p), (lds_void_t*)(L.r + 1024 * k), 16, 0, 0);
+			else
+				*(uint4*)(L.r + 1024 * k + 16 * lane) = stage_piece(make_uint4(0u, 0u, 0u, 0u), R, p, J.rl);
 		}
-		lds_order();
-		if (j + 1 < j1) stage_load(a, j + 1, S);
-		member_chunk(a, L, j);
+		vm_drain();
+		__syncthreads();
 	}
+	member_chunk(a, L, J);
 }
 
 // ── member-mode serialisation ──────────────────────────────────────────
@@ -582,39 +657,32 @@ constexpr uint32_t kSerWavesPerCu = 16;
 
 // one job's inputs, loaded a job ahead (descriptors wave-uniform)
 struct SerFetch {
-	uint32_t pair, c, cnt, boff, first, vl;
+	JobCursor J;
+	uint32_t cnt, boff, first;
 	int32_t st;
 	uint64_t base, end, slot0;
-	const uint8_t* V;
 	uint4 v[kStageRows];   // the chunk's staged V bytes (as the member kernel's)
 	uint4 r;               // member record of this lane (first 64)
 };
 
-__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, uint32_t j, SerFetch& F) {
+// every load unconditional (no branch for the compiler to drain before the
+// loads of the job after it are issued)
+__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
 	const uint32_t lane = lane_id();
-	const uint2 jb = a.chunks[j];
-	F.pair = jb.x;
-	F.c = jb.y;
-	const PairDev pd = a.pairs[F.pair];
-	const PairPlanDev pp = a.pplan[F.pair];
-	F.vl = (uint32_t)pd.v_len;
-	F.V = a.ver + pd.v_off;
-	F.st = a.status[F.pair];
-	F.base = a.offsets[F.pair];
-	F.end = a.offsets[F.pair + 1];
-	const uint2 cm = *(const uint2*)(a.cmap + 2ull * (pp.chunk_base + F.c));
+	const JobCursor& J = F.J;
+	F.st = a.status[J.pair];
+	F.base = a.offsets[J.pair];
+	F.end = a.offsets[J.pair + 1];
+	const uint2 cm = *(const uint2*)(a.cmap + 2ull * (J.chunk_base + J.c));
 	F.cnt = cm.x;
 	F.boff = cm.y;
-	F.slot0 = pp.mem_base + (uint64_t)F.c * kMemChunkSlots;
-	F.first = 0;
-	F.r = make_uint4(0u, 0u, 0u, 0u);
-	if (F.cnt && F.st == 0) {
-		const int64_t g0 = (int64_t)F.c * kMemChunk - 16;
+	F.slot0 = J.mem_base + (uint64_t)J.c * kMemChunkSlots;
+	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
+	const uint8_t* V = a.ver + J.v_off;
 #pragma unroll
-		for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_tail(F.V, g0 + 1024 * k + 16 * lane, F.vl);
-		if (lane < F.cnt) F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));
-		F.first = a.mem_s[F.slot0];
-	}
+	for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
+	F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));   // (slots 0..63 of the chunk's 129)
+	F.first = a.mem_s[F.slot0];
 }
 
 // Member-mode serialisation: each chunk's job writes its bulk piece (the
@@ -629,21 +697,31 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 	const uint32_t lane = lane_id();
 	const uint32_t j0 = (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
 	const uint32_t j1 = (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
+	if (j0 >= j1) return;
 	SerFetch F, N;
-	if (j0 < j1) ser_fetch(a, j0, F);
+	F.J.start(a, j0);
+	ser_fetch(a, F);
 	for (uint32_t j = j0; j < j1; ++j) {
-		if (j + 1 < j1) ser_fetch(a, j + 1, N);
+		if (j + 1 < j1) {
+			N.J = F.J;
+			N.J.next(a);
+			ser_fetch(a, N);
+		}
+		const uint32_t vl = F.J.vl;
+		const uint8_t* V = a.ver + F.J.v_off;
 		if (F.st == 0) {
 			if (F.end > a.out_cap) {
-				if (F.c == 0 && lane == 0) a.status[F.pair] = 7;
+				if (F.J.c == 0 && lane == 0) a.status[F.J.pair] = 7;
 			} else {
 				uint8_t* out = a.out + F.base;
-				if (F.c == 0) put_header(out, F.vl);
+				if (F.J.c == 0) put_header(out, vl);
 				if (F.cnt) {
-					const int64_t g0 = (int64_t)F.c * kMemChunk - 16;
+					const int64_t g0 = (int64_t)F.J.c * kMemChunk - 16;
 					lds_order();
 #pragma unroll
-					for (uint32_t k = 0; k < kStageRows; ++k) *(uint4*)(vbuf + 1024 * k + 16 * lane) = F.v[k];
+					for (uint32_t k = 0; k < kStageRows; ++k)
+						if (1024 * k + 16 * lane < kStage)
+							*(uint4*)(vbuf + 1024 * k + 16 * lane) = stage_piece(F.v[k], V, g0 + 1024 * k + 16 * lane, vl);
 					lds_order();
 					const uint8_t* vb = vbuf;
 					uint64_t pos = F.boff;
@@ -688,19 +766,18 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 				}
 				// the chain's own record runs and the tail (segments 2c, 2c + 1;
 				// the pair's last chunk takes the rest)
-				const PairPlanDev& pp = a.pplan[F.pair];
-				const uint32_t ns = a.nseg[F.pair];
-				const uint32_t* seg = a.seg + 4ull * ((uint64_t)pp.chunk_base + 2ull * F.pair);
-				const uint32_t k1 = F.c + 1 == pp.n_chunks ? ns : umin32(2 * F.c + 2, ns);
-				for (uint32_t k = 2 * F.c; k < k1; ++k) {
+				const uint32_t ns = a.nseg[F.J.pair];
+				const uint32_t* seg = a.seg + 4ull * ((uint64_t)F.J.chunk_base + 2ull * F.J.pair);
+				const uint32_t k1 = F.J.c + 1 == F.J.n_chunks ? ns : umin32(2 * F.J.c + 2, ns);
+				for (uint32_t k = 2 * F.J.c; k < k1; ++k) {
 					const uint4 e = *(const uint4*)(seg + 4ull * k);
 					uint8_t* o = out + e.z;
 					if (e.x == kSegTail) {
-						const uint64_t n = put_tail(o, F.V, F.vl, e.w);
-						if (e.z + n != F.end - F.base && lane == 0) a.status[F.pair] = 5;   // sizes disagree
+						const uint64_t n = put_tail(o, V, vl, e.w);
+						if (e.z + n != F.end - F.base && lane == 0) a.status[F.J.pair] = 5;   // sizes disagree
 					} else {
-						const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (pp.rec_base + e.x), kRecWordsOnepass};
-						serialize_run<kMemSerStage, 1>(o, F.V, F.vl, src, e.y, e.w, (sw_lds8*)stage);
+						const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (F.J.rec_base + e.x), kRecWordsOnepass};
+						serialize_run<kMemSerStage, 1>(o, V, vl, src, e.y, e.w, (sw_lds8*)stage);
 					}
 				}
 			}
@@ -711,8 +788,8 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {
 	if (n_chunks == 0) return hipSuccess;
-	const uint32_t waves = std::min<uint32_t>(n_chunks, kMemWavesPerCu * std::max(n_cu, 1u));
-	hipLaunchKernelGGL(member_chunk_kernel, dim3(waves), dim3(64), 0, st, a, n_chunks);
+	(void)n_cu;
+	hipLaunchKernelGGL(member_chunk_kernel, dim3(n_chunks), dim3(64), 0, st, a, n_chunks);
 	return hipGetLastError();
 }
 

@@ -41,7 +41,7 @@
 
 #define SM_MAX_T 512   /* members of T + 1 > 512 steps are left to the exact engine */
 #define SM_CHUNK 2048  /* member_chunk_kernel: members belong to the chunk of their start ... */
-#define SM_AHEAD 1008  /* ... and need the next member's start within this look-ahead */
+#define SM_AHEAD 240   /* ... and need the next member's start within this look-ahead */
 
 typedef struct {
 	uint64_t members, verified, exact_epochs, resyncs;
