@@ -351,7 +351,7 @@ struct dg_encode_plan {
 	hipEvent_t* cur = nullptr;   // event set of the run being enqueued
 };
 
-static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total"};
+static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total", "members"};
 
 extern "C" {
 
@@ -636,7 +636,7 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 	return P ? P->d_nrec.as<uint32_t>() : nullptr;
 }
 
-constexpr int kTimingEvents = 6;
+constexpr int kTimingEvents = 7;
 
 int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
@@ -657,25 +657,26 @@ int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 }
 
 // Per-run events: 0/1 around the CRC kernels (side stream), 2/3 around the
-// differencing kernel, 4 after the scan, 5 after serialisation + the CRC join
-// + the header patch (DG_SER_BLOCK=1 / DG_FUSED=1: the join falls before 4).
+// differencing kernel(s), 4 after the scan, 5 after serialisation + the CRC
+// join + the header patch (DG_SER_BLOCK=1 / DG_FUSED=1: the join falls before
+// 4), 6 after the member kernel (member mode; else with 2).
 // Returns the mean over the runs recorded since set_timing (at most `slots`).
 int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
 	if (!P || !P->slots || !P->runs) return 0;
 	const uint32_t used = std::min(P->runs, P->slots);
-	const int pairs[5][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}};
-	double acc[5] = {};
+	const int pairs[6][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}, {2, 6}};
+	double acc[6] = {};
 	for (uint32_t s = 0; s < used; ++s) {
 		hipEvent_t* e = &P->ev[(size_t)kTimingEvents * s];
 		if (hipEventSynchronize(e[5]) != hipSuccess) return 0;
-		for (int k = 0; k < 5; ++k) {
+		for (int k = 0; k < 6; ++k) {
 			float t = 0;
 			hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]);
 			acc[k] += t;
 		}
 	}
 	int k = 0;
-	for (; k < 5 && k < n; ++k) {
+	for (; k < 6 && k < n; ++k) {
 		if (ms) ms[k] = (float)(acc[k] / used);
 		if (names) names[k] = kStageNames[k];
 	}
@@ -726,6 +727,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// differencing -> COPY records + per-pair delta sizes
 	auto run_diff = [&]() -> int {
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[2], st));
+		if (P->timing && !P->members) HIPCHK(ctx, hipEventRecord(P->cur[6], st));
 		EncodeArgs a{};
 		a.ref = d_ref;
 		a.ver = d_ver;
@@ -766,6 +768,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				m.csum = P->d_csum.as<uint32_t>();
 				m.cmap = P->d_cmap.as<uint32_t>();
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
+				if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[6], st));
 				a.csum = m.csum;
 				a.cmap = m.cmap;
 				a.seg = P->d_seg.as<uint32_t>();

@@ -186,7 +186,8 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
  * makes every run record its events into one of `slots` event sets (a ring;
  * 0 disables) and resets the run count; dg_encode_plan_stage_times fills up to
  * `n` stage durations (ms), averaged over the last min(runs, slots) runs, and
- * their names ("crc64", "diff", "scan", "serialize+join", "total").  Returns
+ * their names ("crc64", "diff", "scan", "serialize+join", "total", "members";
+ * "members" is the member kernel alone, inside "diff", 0 in plain chain mode).  Returns
  * the number of stages.  No host synchronisation happens until stage_times. */
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,

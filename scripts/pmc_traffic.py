@@ -34,7 +34,7 @@ res = {
     "correction": "FETCH_SIZE x 1024 x 2 (gfx950 counts half of 16 B/lane streaming reads); "
                   "WRITE_SIZE x 1024",
     "command": f"rocprofv3 --pmc <counter> --kernel-include-regex {kre} -- python3 bench.py "
-               f"--config {cfg} --steps 5 --warmup 1 --no-cpu-baseline",
+               f"--config {cfg} --also none --steps 5 --warmup 1 --no-cpu-baseline",
 }
 os.makedirs("profiles", exist_ok=True)
 path = f"profiles/{tag}_pmc_traffic_{cfg}.json"

@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv \
-      -d $OUT/$c -o pmc -- python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline \
+      -d $OUT/$c -o pmc -- python3 bench.py --config $CFG --also none --steps 5 --warmup 1 --no-cpu-baseline \
       > $OUT/$c.log 2>&1 || { echo "pass $c failed rc=$?"; tail -5 $OUT/$c.log; exit 1; }
 done
 python3 scripts/pmc_traffic.py $OUT $TAG $CFG "$KRE"
