@@ -338,6 +338,7 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
+	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	uint64_t qmin = ~0ull;
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
@@ -590,6 +591,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = ab_env("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
+	const char* sk = ab_env("DG_SKIP_CRC");
+	P->skip_crc = sk && sk[0] == '1';
 	{
 		const char* cb = ab_env("DG_CORR_BUILD");
 		int shm = 0;
@@ -720,7 +723,8 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		// waves (16 per CU), so the CRC neither crowds one round out nor
 		// trails a multi-round batch (C2: 4096 pairs -> 512 blocks)
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
-		HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
+		if (!P->skip_crc)
+			HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[1], cs));
 		return DG_OK;
 	};
