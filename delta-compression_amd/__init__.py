@@ -7,6 +7,7 @@ Names and argument meanings follow the reference's interface for this path:
   src/python/delta.py:1579-1629): CRC-64/XZ of both buffers, onepass or
   correcting differencing, placement, DLT\\x03 serialisation.
 * ``encode_batch(pairs, ...)``      — the same for many pairs at once.
+* ``encode_pipelined(pairs, ...)``  — host arenas in chunks, H2D / encode / D2H overlapped.
 * ``EncodePlan``                    — device-resident batches (the hot path).
 * ``crc64_xz(data)``                — ``delta_crc64_xz`` (src/c/delta.h:294).
 * ``decode(R, delta)``              — ``delta decode`` (main.c:323-400).
@@ -42,6 +43,7 @@ from ._lib import (  # noqa: F401
     default_context,
     encode,
     encode_batch,
+    encode_pipelined,
     info,
     lib,
     make_inplace,
@@ -51,7 +53,7 @@ from ._lib import (  # noqa: F401
 __all__ = [
     "ALGO_ONEPASS", "ALGO_CORRECTING", "ALGO_GREEDY", "SEED_LEN", "TABLE_SIZE",
     "MAX_TABLE_SIZE", "BUF_CAP", "Context", "DeltaError", "DiffOptions", "EncodePlan", "DecodePlan",
-    "crc64_xz", "decode", "default_context", "encode", "encode_batch", "info", "lib",
+    "crc64_xz", "decode", "default_context", "encode", "encode_batch", "encode_pipelined", "info", "lib",
     "make_inplace", "status_string", "LIB_PATH", "LIMIT_TABLE_POOL_BYTES",
     "LIMIT_ONEPASS_MEMBERS", "MEMBERS_AUTO", "MEMBERS_ON", "MEMBERS_OFF",
 ]

@@ -133,6 +133,10 @@ def _load() -> C.CDLL:
         "dg_encode_batch": (C.c_int, [vp, C.c_int, C.POINTER(u8p), C.POINTER(sz), C.POINTER(u8p),
                                       C.POINTER(sz), u32, C.POINTER(DiffOptions), C.POINTER(Buffer),
                                       C.POINTER(i32)]),
+        "dg_encode_pipelined": (C.c_int, [vp, C.c_int, vp, vp, C.POINTER(Pair), u32, C.POINTER(DiffOptions), u64,
+                                          vp, u64, C.POINTER(u64), C.POINTER(i32)]),
+        "dg_host_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "dg_host_free": (None, [vp]),
         "dg_crc64_xz": (C.c_int, [vp, u8p, sz, C.c_uint8 * 8]),
         "dg_crc64_xz_batch_device": (C.c_int, [vp, vp, C.POINTER(Span), u32, vp, vp]),
         "dg_decode": (C.c_int, [vp, u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer)]),
@@ -375,6 +379,58 @@ def encode_batch(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: i
         res.append(C.string_at(outs[i].data, outs[i].len))
         lib.dg_buffer_free(C.byref(outs[i]))
     return res
+
+
+def encode_pipelined(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: int = SEED_LEN,
+                     q: int = TABLE_SIZE, buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE,
+                     chunk_bytes: int = 0, pinned: bool = False, align: int = 16, out_cap: Optional[int] = None,
+                     ctx: Optional[Context] = None) -> List[bytes]:
+    """Many pairs host-to-host through dg_encode_pipelined (chunked, two chunks in
+    flight).  The pairs are laid out in host arenas `align` bytes apart, pinned
+    (dg_host_alloc) or pageable (bytearray)."""
+    ctx = ctx or default_context()
+    n = len(pairs)
+    if n == 0:
+        return []
+    lay, rt, vt = [], 0, 0
+    for r, v in pairs:   # each pair at the next multiple of `align` (1: packed, unaligned)
+        ro, vo = (rt + align - 1) // align * align, (vt + align - 1) // align * align
+        lay.append((ro, len(r), vo, len(v)))
+        rt, vt = ro + len(r), vo + len(v)
+    cap = out_cap if out_cap is not None else sum(len(v) for _, v in pairs) + 64 * n + 64
+    bufs = []
+
+    def host(nbytes):
+        if pinned:
+            h = C.c_void_p()
+            ctx.check(lib.dg_host_alloc(ctx.handle, max(nbytes, 1), C.byref(h)), "dg_host_alloc")
+            bufs.append(h)
+            return h.value
+        b = (C.c_uint8 * max(nbytes, 1))()
+        bufs.append(b)
+        return C.addressof(b)
+
+    try:
+        hr, hv, ho = host(rt), host(vt), host(cap)
+        for (r, v), (ro, _, vo, _) in zip(pairs, lay):
+            C.memmove(hr + ro, bytes(r), len(r))
+            C.memmove(hv + vo, bytes(v), len(v))
+        pa = (Pair * n)(*[Pair(*x) for x in lay])
+        offs = (C.c_uint64 * (n + 1))()
+        st = (C.c_int32 * n)()
+        o = _opts(p, q, buf_cap, max_table)
+        ctx.check(lib.dg_encode_pipelined(ctx.handle, _algo(algorithm), hr, hv, pa, n, C.byref(o), chunk_bytes,
+                                          ho, cap, offs, st), "dg_encode_pipelined")
+        res = []
+        for i in range(n):
+            if st[i]:
+                raise DeltaError(st[i], f"pair {i}")
+            res.append(C.string_at(ho + offs[i], offs[i + 1] - offs[i]))
+        return res
+    finally:
+        if pinned:
+            for h in bufs:
+                lib.dg_host_free(h)
 
 
 def make_inplace(R: bytes, delta: bytes, policy: str = "localmin", stats: bool = False):

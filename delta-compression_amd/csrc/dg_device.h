@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+typedef struct dg_context dg_context_t;
+
 namespace dg {
 
 constexpr uint64_t kMersenne = (1ULL << 61) - 1;   // src/c/delta.h:25
@@ -214,6 +216,8 @@ struct SynthCopy {   // V[dst..+len) = R[src..+len)
 // library, which therefore reads no environment variable that changes the
 // work it does (dg_host.cpp).
 const char* ab_env(const char* name);
+// the context's slot for the pipelined host path's state, and its destructor
+void** ctx_io(dg_context_t* ctx, void (*release)(void*));
 
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);

@@ -114,7 +114,14 @@ struct dg_context {
 	// scratch reused by the host-buffer entry points
 	void* pin = nullptr;
 	size_t pin_cap = 0;
+	void* io = nullptr;                 // dg_encode_pipelined's slots (dg_host_io.cpp)
+	void (*io_free)(void*) = nullptr;
 };
+
+void** dg::ctx_io(dg_context_t* ctx, void (*release)(void*)) {
+	ctx->io_free = release;
+	return &ctx->io;
+}
 
 static int set_err(dg_context_t* ctx, int code, const char* fmt, ...) {
 	if (ctx) {
@@ -237,6 +244,7 @@ void dg_context_destroy(dg_context_t* ctx) {
 	hipFree(ctx->d_crc_tables);
 	hipFree(ctx->d_xinv);
 	if (ctx->pin) hipHostFree(ctx->pin);
+	if (ctx->io && ctx->io_free) ctx->io_free(ctx->io);
 	if (ctx->stream) hipStreamDestroy(ctx->stream);
 	delete ctx;
 }

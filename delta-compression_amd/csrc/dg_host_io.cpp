@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/delta_gpu.h"
@@ -18,14 +19,16 @@ namespace {
 
 struct Dev {
 	void* p = nullptr;
-	~Dev() { if (p) hipFree(p); }
+	~Dev() { reset(); }
+	void reset() { if (p) hipFree(p); p = nullptr; }
 	bool alloc(size_t n) { return hipMalloc(&p, n ? n : 16) == hipSuccess; }
 	template <class T> T* as() { return static_cast<T*>(p); }
 };
 
 struct Pinned {
 	void* p = nullptr;
-	~Pinned() { if (p) hipHostFree(p); }
+	~Pinned() { reset(); }
+	void reset() { if (p) hipHostFree(p); p = nullptr; }
 	bool alloc(size_t n) { return hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault) == hipSuccess; }
 	template <class T> T* as() { return static_cast<T*>(p); }
 };
@@ -138,6 +141,259 @@ int dg_encode_batch(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* const
 		outs[i].len = len;
 	}
 	return status ? DG_OK : first_bad;
+}
+
+// ── pipelined host-to-host encode ──────────────────────────────────────
+//
+// Two slots, each with its own stream, device buffers, plan and pinned
+// staging, kept in the context between calls.  Per chunk (consecutive pairs,
+// about chunk_bytes of input): [stage the inputs into pinned memory when the
+// caller's arenas are pageable] -> H2D -> dg_encode_plan_run -> D2H of the
+// offsets and status -> (when the slot is next needed) D2H of exactly the
+// chunk's delta bytes.  Chunk i+1's copies run while chunk i encodes.
+}  // extern "C"
+
+namespace {
+
+bool host_pinned(const void* p) {
+	if (!p) return false;
+	hipPointerAttribute_t at{};
+	if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+		(void)hipGetLastError();   // pageable memory reports an error: clear it
+		return false;
+	}
+	return at.type == hipMemoryTypeHost;
+}
+
+struct IoSlot {
+	hipStream_t s = nullptr;
+	hipEvent_t ev = nullptr;
+	dg_encode_plan_t* plan = nullptr;
+	std::vector<dg_pair_t> key;   // the plan's layout (chunk-relative)
+	dg_algorithm_t key_algo = DG_ALGO_ONEPASS;
+	dg_diff_options_t key_opts{};
+	Dev d_ref, d_ver, d_out, d_off, d_st;
+	uint64_t cap_ref = 0, cap_ver = 0, cap_out = 0, cap_doff = 0, cap_dst = 0;
+	Pinned h_in, h_out, h_off, h_st;
+	uint64_t cap_hin = 0, cap_hout = 0, cap_hoff = 0, cap_hst = 0;
+	// the chunk in flight
+	bool pending = false;
+	uint32_t p0 = 0, p1 = 0;      // its pairs
+	uint64_t bound = 0;
+	~IoSlot() {
+		if (plan) dg_encode_plan_destroy(plan);
+		if (ev) hipEventDestroy(ev);
+		if (s) hipStreamDestroy(s);
+	}
+};
+
+struct IoState {
+	IoSlot slot[2];
+};
+
+void io_release(void* p) { delete static_cast<IoState*>(p); }
+
+// memcpy for pageable <-> pinned staging, split over a few host threads (one
+// thread copies ~10 GB/s, PCIe moves ~50): pieces of >= 8 MiB
+void par_memcpy(void* dst, const void* src, uint64_t n) {
+	const uint64_t kPiece = 8ull << 20;
+	unsigned t = std::thread::hardware_concurrency();
+	t = std::max(1u, std::min(8u, t));
+	const uint64_t parts = std::min<uint64_t>(t, (n + kPiece - 1) / kPiece);
+	if (parts <= 1) {
+		memcpy(dst, src, n);
+		return;
+	}
+	std::vector<std::thread> th;
+	const uint64_t per = (n + parts - 1) / parts;
+	for (uint64_t k = 1; k < parts; ++k) {
+		const uint64_t a = k * per, b = std::min(n, a + per);
+		if (a < b) th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
+	}
+	memcpy(dst, src, std::min(n, per));
+	for (auto& x : th) x.join();
+}
+
+template <class B>
+bool grow(B& b, uint64_t& cap, uint64_t need) {
+	if (need <= cap && b.p) return true;
+	b.reset();
+	cap = 0;
+	if (!b.alloc(need)) return false;
+	cap = need;
+	return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dg_host_alloc(dg_context_t* ctx, uint64_t bytes, void** out) {
+	if (!ctx || !out) return DG_ERR_INVALID_ARG;
+	*out = nullptr;
+	return hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault) == hipSuccess ? DG_OK : DG_ERR_NOMEM;
+}
+
+void dg_host_free(void* p) {
+	if (p) hipHostFree(p);
+}
+
+int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h_ref, const uint8_t* h_ver,
+                        const dg_pair_t* pairs, uint32_t n, const dg_diff_options_t* opts,
+                        uint64_t chunk_bytes, uint8_t* h_out, uint64_t out_cap, uint64_t* out_offsets,
+                        int32_t* status) {
+	if (!ctx || !out_offsets || (n && (!pairs || !h_ref || !h_ver || !h_out))) return DG_ERR_INVALID_ARG;
+	out_offsets[0] = 0;
+	if (n == 0) return DG_OK;
+	if (opts && ((opts->flags >> DG_OPT_INPLACE) & 1)) return DG_ERR_UNSUPPORTED;   // host step: dg_encode_batch
+	dg_diff_options_t o;
+	if (opts) o = *opts; else dg_diff_options_default(&o);
+	if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+	void** io = dg::ctx_io(ctx, io_release);
+	if (!*io) *io = new (std::nothrow) IoState();
+	if (!*io) return DG_ERR_NOMEM;
+	IoState& S = *static_cast<IoState*>(*io);
+	for (IoSlot& sl : S.slot) {
+		if (!sl.s && hipStreamCreateWithFlags(&sl.s, hipStreamNonBlocking) != hipSuccess) return DG_ERR_HIP;
+		if (!sl.ev && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) return DG_ERR_HIP;
+		sl.pending = false;
+	}
+	const bool in_pinned = host_pinned(h_ref) && host_pinned(h_ver);
+	const bool out_pinned = host_pinned(h_out);
+
+	// chunks of consecutive pairs
+	std::vector<uint32_t> cuts{0};
+	{
+		uint64_t acc = 0;
+		for (uint32_t i = 0; i < n; ++i) {
+			const uint64_t b = pairs[i].r_len + pairs[i].v_len;
+			if (acc && acc + b > chunk_bytes) {
+				cuts.push_back(i);
+				acc = 0;
+			}
+			acc += b;
+		}
+		cuts.push_back(n);
+	}
+	uint64_t out_pos = 0;
+	int rc_all = DG_OK;
+	bool full = false;
+	std::vector<dg_pair_t> rel;
+
+	// the slot's finished chunk: its delta bytes to h_out, offsets and status
+	auto drain = [&](IoSlot& sl) -> int {
+		if (!sl.pending) return DG_OK;
+		sl.pending = false;
+		if (hipEventSynchronize(sl.ev) != hipSuccess) return DG_ERR_HIP;
+		const uint32_t m = sl.p1 - sl.p0;
+		const uint64_t* off = sl.h_off.as<uint64_t>();
+		const int32_t* st = sl.h_st.as<int32_t>();
+		const uint64_t total = off[m];
+		if (full || out_pos + total > out_cap) {
+			full = true;
+			return DG_OK;
+		}
+		if (total) {
+			if (out_pinned) {
+				if (hipMemcpyAsync(h_out + out_pos, sl.d_out.p, total, hipMemcpyDeviceToHost, sl.s) != hipSuccess)
+					return DG_ERR_HIP;
+			} else {
+				if (!grow(sl.h_out, sl.cap_hout, total)) return DG_ERR_NOMEM;
+				if (hipMemcpyAsync(sl.h_out.p, sl.d_out.p, total, hipMemcpyDeviceToHost, sl.s) != hipSuccess ||
+				    hipStreamSynchronize(sl.s) != hipSuccess)
+					return DG_ERR_HIP;
+				par_memcpy(h_out + out_pos, sl.h_out.p, total);
+			}
+		}
+		for (uint32_t k = 0; k < m; ++k) {
+			out_offsets[sl.p0 + k + 1] = out_pos + off[k + 1];
+			if (status) status[sl.p0 + k] = st[k];
+			if (st[k] && !rc_all) rc_all = st[k];
+		}
+		out_pos += total;
+		return DG_OK;
+	};
+
+	int rc = DG_OK;
+	const uint32_t n_chunks = (uint32_t)cuts.size() - 1;
+	for (uint32_t c = 0; c < n_chunks && rc == DG_OK; ++c) {
+		IoSlot& sl = S.slot[c & 1];
+		if ((rc = drain(sl)) != DG_OK) break;
+		// the slot's previous D2H (issued on its stream) orders before this
+		// chunk's H2D; its pinned staging is reused only after that drain
+		if (hipStreamSynchronize(sl.s) != hipSuccess) { rc = DG_ERR_HIP; break; }
+		const uint32_t p0 = cuts[c], p1 = cuts[c + 1], m = p1 - p0;
+		uint64_t r_lo = ~0ull, r_hi = 0, v_lo = ~0ull, v_hi = 0;
+		for (uint32_t i = p0; i < p1; ++i) {
+			r_lo = std::min<uint64_t>(r_lo, pairs[i].r_off);
+			r_hi = std::max<uint64_t>(r_hi, pairs[i].r_off + pairs[i].r_len);
+			v_lo = std::min<uint64_t>(v_lo, pairs[i].v_off);
+			v_hi = std::max<uint64_t>(v_hi, pairs[i].v_off + pairs[i].v_len);
+		}
+		// keep the arena's 16-byte phase so aligned layouts stay aligned
+		r_lo &= ~15ull;
+		v_lo &= ~15ull;
+		const uint64_t rn = r_hi - r_lo, vn = v_hi - v_lo;
+		rel.resize(m);
+		for (uint32_t i = p0; i < p1; ++i)
+			rel[i - p0] = dg_pair_t{pairs[i].r_off - r_lo, pairs[i].r_len, pairs[i].v_off - v_lo, pairs[i].v_len};
+		const bool same = sl.plan && sl.key_algo == algo && !memcmp(&sl.key_opts, &o, sizeof o) &&
+		                  sl.key.size() == rel.size() && !memcmp(sl.key.data(), rel.data(), m * sizeof(dg_pair_t));
+		if (!same) {
+			if (sl.plan) dg_encode_plan_destroy(sl.plan);
+			sl.plan = nullptr;
+			if ((rc = dg_encode_plan_create(ctx, algo, rel.data(), m, &o, &sl.plan)) != DG_OK) break;
+			sl.key = rel;
+			sl.key_algo = algo;
+			sl.key_opts = o;
+			sl.bound = dg_encode_plan_output_bound(sl.plan);
+		}
+		if (!grow(sl.d_ref, sl.cap_ref, rn) || !grow(sl.d_ver, sl.cap_ver, vn) ||
+		    !grow(sl.d_out, sl.cap_out, sl.bound) || !grow(sl.d_off, sl.cap_doff, 8ull * (m + 1)) ||
+		    !grow(sl.d_st, sl.cap_dst, 4ull * m) || !grow(sl.h_off, sl.cap_hoff, 8ull * (m + 1)) ||
+		    !grow(sl.h_st, sl.cap_hst, 4ull * m)) {
+			rc = DG_ERR_NOMEM;
+			break;
+		}
+		const uint8_t* src_r = h_ref + r_lo;
+		const uint8_t* src_v = h_ver + v_lo;
+		if (!in_pinned) {   // stage: one host copy per stream per chunk
+			if (!grow(sl.h_in, sl.cap_hin, rn + vn)) { rc = DG_ERR_NOMEM; break; }
+			par_memcpy(sl.h_in.p, src_r, rn);
+			par_memcpy(sl.h_in.as<uint8_t>() + rn, src_v, vn);
+			src_r = sl.h_in.as<uint8_t>();
+			src_v = src_r + rn;
+		}
+		if (hipMemcpyAsync(sl.d_ref.p, src_r, rn, hipMemcpyHostToDevice, sl.s) != hipSuccess ||
+		    hipMemcpyAsync(sl.d_ver.p, src_v, vn, hipMemcpyHostToDevice, sl.s) != hipSuccess) {
+			rc = DG_ERR_HIP;
+			break;
+		}
+		if ((rc = dg_encode_plan_run(sl.plan, sl.d_ref.as<uint8_t>(), sl.d_ver.as<uint8_t>(), sl.d_out.as<uint8_t>(),
+		                             sl.bound, sl.d_off.as<uint64_t>(), sl.d_st.as<int32_t>(), sl.s)) != DG_OK)
+			break;
+		if (hipMemcpyAsync(sl.h_off.p, sl.d_off.p, 8ull * (m + 1), hipMemcpyDeviceToHost, sl.s) != hipSuccess ||
+		    hipMemcpyAsync(sl.h_st.p, sl.d_st.p, 4ull * m, hipMemcpyDeviceToHost, sl.s) != hipSuccess ||
+		    hipEventRecord(sl.ev, sl.s) != hipSuccess) {
+			rc = DG_ERR_HIP;
+			break;
+		}
+		sl.pending = true;
+		sl.p0 = p0;
+		sl.p1 = p1;
+		// the other slot's chunk (one behind) goes out while this one encodes
+		if ((rc = drain(S.slot[(c + 1) & 1])) != DG_OK) break;
+	}
+	// in chunk order: the slot holding the older chunk first
+	if (rc == DG_OK && n_chunks >= 2) rc = drain(S.slot[n_chunks & 1]);
+	if (rc == DG_OK) rc = drain(S.slot[(n_chunks - 1) & 1]);
+	for (IoSlot& sl : S.slot) {
+		hipStreamSynchronize(sl.s);
+		sl.pending = false;
+	}
+	if (rc != DG_OK) return rc;
+	if (full) return DG_ERR_CAPACITY;
+	return status ? DG_OK : rc_all;
 }
 
 int dg_encode(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* r, size_t r_len,

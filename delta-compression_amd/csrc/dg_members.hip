@@ -55,7 +55,6 @@ constexpr uint32_t kStage = kMemChunk + kMemAhead + 16;   // staged bytes per st
 constexpr uint32_t kMaskWords = (kStage + 31) / 32;        // mismatch bitmap words
 constexpr uint32_t kRunList = kStage / 17 + 4;             // run starts in the staged region (>= 17 apart)
 constexpr uint32_t kLongChunks = 8;
-constexpr uint32_t kMemWavesPerCu = 16;
 #ifndef DG_MEM_WAVES
 #define DG_MEM_WAVES 7   // minimum waves per SIMD the register budget must allow
 #endif                    // persistent waves (LDS allows 17)                        // members of up to 512 steps are verified
@@ -322,7 +321,7 @@ __device__ __forceinline__ void stage_store(const SpecArgs& a, const JobCursor& 
 
 __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, const JobCursor& J) {
 	const uint32_t lane = lane_id();
-	const uint32_t pair = J.pair, c = J.c;
+	const uint32_t c = J.c;
 	const uint32_t vl = J.vl, rl = J.rl;
 	const uint32_t E = umin32(vl, rl);
 	const uint32_t cw = c * kMemChunk;                  // chunk start (position)

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define DG_ABI_VERSION 2
+#define DG_ABI_VERSION 3
 
 /* Defaults mirror src/c/delta.h:21-35. */
 #define DG_SEED_LEN        16
@@ -217,6 +217,33 @@ int dg_encode_batch(dg_context_t *ctx, dg_algorithm_t algo,
                     const uint8_t *const *v, const size_t *v_len,
                     uint32_t n_pairs, const dg_diff_options_t *opts,
                     dg_buffer_t *outs, int32_t *status);
+
+/* ── Pipelined host-to-host batch encode ──────────
+ * The reference's encode reads R and V from host files and writes the delta
+ * back (main.c:33-121, 249-292).  For n pairs in host arenas h_ref / h_ver,
+ * laid out by pairs[] as for dg_encode_plan_create, this cuts the batch into
+ * chunks of consecutive pairs of about chunk_bytes of input each (0: 256 MiB)
+ * and keeps two chunks in flight on two streams: the H2D copy of chunk i+1
+ * and the D2H copy of chunk i-1's exact delta bytes overlap the encode of
+ * chunk i.  The deltas land in h_out (out_cap bytes) packed in pair order,
+ * delta i at out_offsets[i] .. out_offsets[i+1] (host, n+1 entries); status[i]
+ * per pair (host, may be NULL).  Arenas and h_out from dg_host_alloc (pinned)
+ * are copied directly; other host memory goes through pinned staging that
+ * the context keeps between calls, as are the device buffers and plans (a
+ * chunk with the same layout as the slot's last one reuses its plan).
+ * Returns DG_OK (per-pair failures in status), DG_ERR_CAPACITY when h_out is
+ * too small (out_offsets then hold the bytes written so far), or the first
+ * failure when status is NULL. */
+int dg_encode_pipelined(dg_context_t *ctx, dg_algorithm_t algo,
+                        const uint8_t *h_ref, const uint8_t *h_ver,
+                        const dg_pair_t *pairs, uint32_t n_pairs,
+                        const dg_diff_options_t *opts, uint64_t chunk_bytes,
+                        uint8_t *h_out, uint64_t out_cap,
+                        uint64_t *out_offsets, int32_t *status);
+
+/* Pinned (page-locked) host memory for the arenas and outputs above. */
+int  dg_host_alloc(dg_context_t *ctx, uint64_t bytes, void **out);
+void dg_host_free(void *p);
 
 /* ── CRC-64/XZ (delta.h:294-322), computed on the device ──────────────── */
 

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol(dg):
 
 
 def test_abi_version(dg):
-    assert dg.lib.dg_abi_version() == 2
+    assert dg.lib.dg_abi_version() == 3
 
 
 def test_product_library_reads_no_environment(dg):
