@@ -86,6 +86,14 @@ __device__ __forceinline__ bool checkpoint_slot(uint64_t fp, const PairPlanDev& 
 	return r == k && i < pp.q;
 }
 
+// the checkpoint test alone (f mod m == k), whether or not f / m is a slot
+// (--verbose counts it as the reference does, correcting.c:173, 242)
+__device__ __forceinline__ bool checkpoint_only(uint64_t fp, const PairPlanDev& pp, uint64_t k, uint64_t* slot) {
+	const uint64_t f = mod_q(fp, pp.f_size, pp.f_magic);
+	*slot = f / pp.m;
+	return f % pp.m == k;
+}
+
 // Extensions compare 4 KiB per wave step: 4 chunks of 16 bytes per lane,
 // all loads issued before any compare (the byte streams come from HBM/L2,
 // so a step is one load latency rather than four).
@@ -204,6 +212,37 @@ __global__ __launch_bounds__(64) void correcting_class_kernel(EncodeArgs a) {
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
 	a.kcls[pair] = checkpoint_class(a.ver + pd.v_off, pd.v_len, a.p, a.pplan[pair]);
+	if (a.stats) a.stats[8ull * pair + 6] = a.kcls[pair];
+}
+
+// --verbose only (a.stats): the build's counts, recomputed apart from the
+// build kernels so they carry no counters — seeds passing the checkpoint
+// test (correcting.c:174) and the slots they filled (first-found policy:
+// stored = occupied slots, collisions = passed - stored, :176-196)
+__global__ __launch_bounds__(256) void correcting_stats_kernel(EncodeArgs a) {
+	const uint32_t pair = blockIdx.x;
+	const PairPlanDev pp = a.pplan[pair];
+	const PairDev pd = a.pairs[pair];
+	const uint32_t p = a.p;
+	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
+	unsigned long long passed = 0, in_cap = 0, stored = 0;
+	if (pd.v_len > 0) {
+		const uint64_t k = a.kcls[pair];
+		const uint8_t* R = a.ref + pd.r_off;
+		for (uint64_t s = threadIdx.x; s < seeds; s += 256) {
+			const uint64_t fp = window_fp<0>(R + s, p, a.powc);
+			uint64_t slot;
+			if (checkpoint_only(fp, pp, k, &slot)) {
+				++passed;
+				in_cap += slot < pp.q ? 1u : 0u;
+			}
+		}
+		const uint32_t* H = a.ctab + pp.tab_base;
+		for (uint64_t i = threadIdx.x; i < pp.q; i += 256) stored += H[i] != kNone ? 1u : 0u;
+	}
+	if (passed) atomicAdd((unsigned long long*)&a.stats[8ull * pair + 0], passed);
+	if (stored) atomicAdd((unsigned long long*)&a.stats[8ull * pair + 1], stored);
+	if (in_cap) atomicAdd((unsigned long long*)&a.stats[8ull * pair + 7], in_cap);
 }
 
 __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a, uint32_t nchunk,
@@ -426,10 +465,11 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 		const uint64_t k = uni64(a.kcls[pair]);
 		const Ckpt ck = make_ckpt(pp.f_size, pp.f_magic, pp.m, k, pp.q);
 		uint32_t vc = 0, vs = 0;
+		uint64_t n_ck = 0, n_fpm = 0, n_bm = 0, n_match = 0;   // --verbose counters (a.stats)
 		while (st == 0 && vc + p <= vl) {
 			// ── positions vc .. vc+63: fingerprint, checkpoint, lookup, memcmp ──
 			const uint32_t pos = vc + lane;
-			bool hit = false;
+			bool hit = false, passed = false, fpm = false, bm = false;
 			uint32_t off = kNone;
 			if (pos + p <= vl) {
 				uint32_t wv[4];
@@ -442,6 +482,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 				}
 				uint32_t slot;
 				if (ck.mf.ok ? ckpt_test(fp, ck, &slot) : checkpoint_slot(fp, pp, k, &slot)) {
+					passed = true;
 					off = H[slot];
 					if (off != kNone) {   // correcting.c:268-285: verify the seed bytes
 						if (p == 16) {
@@ -452,10 +493,25 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 							hit = true;
 							for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
 						}
+						if (a.stats && !hit) {   // the reference's stored-fingerprint test (:254-283)
+							const bool fpeq = window_fp<0>(R + off, p, a.powc) == fp;
+							fpm = !fpeq;
+							bm = fpeq;
+						}
 					}
+				} else if (a.stats) {   // a checkpoint whose f / m is past the table (:242, :268)
+					uint64_t sl;
+					passed = checkpoint_only(fp, pp, k, &sl);
 				}
 			}
 			const uint64_t M = __ballot(hit);
+			if (a.stats) {   // positions the reference visits: up to the first match
+				const uint64_t seen = M ? mask_le(ffs64(M)) : ~0ull;
+				n_ck += __builtin_popcountll(__ballot(passed) & seen);
+				n_fpm += __builtin_popcountll(__ballot(fpm) & seen);
+				n_bm += __builtin_popcountll(__ballot(bm) & seen);
+				n_match += M ? 1u : 0u;
+			}
 			if (!M) { vc += 64; continue; }
 			const uint32_t jf = ffs64(M);
 			vc = uni(vc + jf);
@@ -513,6 +569,12 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 			--n;
 		}
 		if (vs < vl) dsz += 9ull + (vl - vs);
+		if (a.stats && lane == 0) {
+			a.stats[8ull * pair + 2] = n_ck;
+			a.stats[8ull * pair + 3] = n_fpm;
+			a.stats[8ull * pair + 4] = n_bm;
+			a.stats[8ull * pair + 5] = n_match;
+		}
 	}
 	if (lane == 0) {
 		a.n_rec[pair] = nrec;
@@ -542,6 +604,7 @@ hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, ui
 		if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
 		hipLaunchKernelGGL(correcting_build_kernel, dim3((uint32_t)blocks), dim3(kBuildBlock), 0, st, a, nchunk, lds_cap);
 	}
+	if (a.stats) hipLaunchKernelGGL(correcting_stats_kernel, dim3(a.n_pairs), dim3(256), 0, st, a);
 	const size_t lds = sizeof(RingEnt) * ((size_t)(a.buf_cap ? a.buf_cap : 1) + 1);
 	hipLaunchKernelGGL(correcting_scan_kernel, dim3(a.n_pairs), dim3(64), lds, st, a);
 	return hipGetLastError();

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 typedef struct dg_context dg_context_t;
+typedef struct dg_encode_plan dg_encode_plan_t;
 
 namespace dg {
 
@@ -108,6 +109,11 @@ struct EncodeArgs {
 	uint32_t* cmap;
 	uint32_t* seg;
 	uint32_t* nseg;            // per pair: segments written
+	// --verbose diagnostics (correcting; nullptr = off): per pair 8 u64 —
+	// build seeds passing the checkpoint, slots stored, scan checkpoints, fp
+	// mismatches, byte mismatches, matches, k, passing seeds whose slot is in
+	// the table (correcting.c:95-98, 137-214, 470-485)
+	uint64_t* stats;
 };
 
 constexpr uint32_t kSegTail = 0xFFFFFFFFu;
@@ -218,6 +224,11 @@ struct SynthCopy {   // V[dst..+len) = R[src..+len)
 const char* ab_env(const char* name);
 // the context's slot for the pipelined host path's state, and its destructor
 void** ctx_io(dg_context_t* ctx, void (*release)(void*));
+// --verbose: the reference's diagnostic lines for pair i of a plan to stderr,
+// from the plan's parameters, its 8 device counters (copied to the host; may
+// be NULL for onepass) and the pair's delta (dg_host.cpp)
+void print_verbose(const dg_encode_plan_t* P, uint32_t i, const uint64_t* stats, const uint8_t* delta,
+                   size_t delta_len);
 
 // launchers (dg_kernels.hip)
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);

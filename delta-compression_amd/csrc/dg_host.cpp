@@ -348,6 +348,7 @@ struct dg_encode_plan {
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
+	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
 	bool ser_block = false;    // DG_SER_BLOCK=1: block-per-pair serialiser (A/B)
@@ -361,6 +362,122 @@ struct dg_encode_plan {
 };
 
 static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total", "members"};
+
+// ── --verbose: the reference's diagnostics from device counters and the delta ──
+
+static uint32_t be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+
+namespace {
+struct Cmd { bool copy; uint64_t src, dst, len; };
+// the standard delta's commands (encoding.c:39-90 layout), in stream order
+bool parse_cmds(const uint8_t* d, size_t n, std::vector<Cmd>& out) {
+	if (n < 26 || memcmp(d, "DLT\x03", 4) != 0) return false;
+	size_t i = 25;
+	while (i < n) {
+		const uint8_t t = d[i];
+		if (t == 0) return true;
+		if (t == 1 && i + 13 <= n) {
+			out.push_back(Cmd{true, be32(d + i + 1), be32(d + i + 5), be32(d + i + 9)});
+			i += 13;
+		} else if (t == 2 && i + 9 <= n) {
+			const uint64_t len = be32(d + i + 5);
+			out.push_back(Cmd{false, 0, be32(d + i + 1), len});
+			i += 9 + len;
+		} else {
+			return false;
+		}
+	}
+	return false;
+}
+
+// delta_print_command_stats (correcting.c:523-576)
+void print_command_stats(const std::vector<Cmd>& cmds) {
+	uint64_t tc = 0, ta = 0, nc = 0, na = 0;
+	std::vector<uint64_t> lens;
+	for (const Cmd& c : cmds) {
+		if (c.copy) { tc += c.len; ++nc; lens.push_back(c.len); }
+		else { ta += c.len; ++na; }
+	}
+	const uint64_t tot = tc + ta;
+	fprintf(stderr,
+	        "  result: %llu copies (%llu bytes), %llu adds (%llu bytes)\n"
+	        "  result: copy coverage %.1f%%, output %llu bytes\n",
+	        (unsigned long long)nc, (unsigned long long)tc, (unsigned long long)na, (unsigned long long)ta,
+	        tot > 0 ? (double)tc / tot * 100.0 : 0.0, (unsigned long long)tot);
+	if (!lens.empty()) {
+		std::sort(lens.begin(), lens.end());
+		fprintf(stderr, "  copies: %llu regions, min=%llu max=%llu mean=%.1f median=%llu bytes\n",
+		        (unsigned long long)lens.size(), (unsigned long long)lens.front(), (unsigned long long)lens.back(),
+		        (double)tc / lens.size(), (unsigned long long)lens[lens.size() / 2]);
+	}
+}
+}  // namespace
+
+void dg::print_verbose(const dg_encode_plan_t* P, uint32_t i, const uint64_t* st, const uint8_t* delta,
+                       size_t delta_len) {
+	const dg_pair_t& d = P->pairs[i];
+	const PairPlanDev& x = P->pp[i];
+	const uint64_t p = P->opts.p;
+	if (d.v_len == 0) return;   // the reference returns before printing (onepass.c:58, correcting.c:112)
+	std::vector<Cmd> cmds;
+	parse_cmds(delta, delta_len, cmds);
+	if (P->algo == DG_ALGO_ONEPASS) {
+		// onepass.c:64-69 and :277-285.  positions: every epoch's steps up to
+		// its match (t + 1, t = max(v_m - v0, r_m - r0)) plus the final
+		// epoch's steps while either stream has a window; lookups: one per
+		// match (a probe counts only on a full-fingerprint hit, onepass.c:169-
+		// 219, and fingerprints of distinct 16-byte windows coincide with
+		// probability ~2^-61)
+		fprintf(stderr, "onepass: %s, q=%llu, |R|=%llu, |V|=%llu, seed_len=%llu\n", "hash table",
+		        (unsigned long long)x.q, (unsigned long long)d.r_len, (unsigned long long)d.v_len,
+		        (unsigned long long)p);
+		uint64_t pos = 0, matches = 0, v0 = 0, r0 = 0;
+		for (const Cmd& c : cmds) {
+			if (!c.copy) continue;
+			pos += std::max(c.dst - v0, c.src - r0) + 1;
+			++matches;
+			v0 = c.dst + c.len;
+			r0 = c.src + c.len;
+		}
+		const uint64_t nv = d.v_len + 1 >= v0 + p ? d.v_len + 1 - p - v0 : 0;
+		const uint64_t nr = d.r_len + 1 >= r0 + p ? d.r_len + 1 - p - r0 : 0;
+		pos += std::max(nv, nr);
+		fprintf(stderr,
+		        "  scan: %llu positions, %llu lookups, %llu matches (flushes)\n"
+		        "  scan: hit rate %.1f%% (of lookups)\n",
+		        (unsigned long long)pos, (unsigned long long)matches, (unsigned long long)matches,
+		        matches > 0 ? 100.0 : 0.0);
+		print_command_stats(cmds);
+		return;
+	}
+	// correcting.c:137-152, 200-214, 470-485
+	const uint64_t seeds = d.r_len >= p ? d.r_len - p + 1 : 0;
+	const uint64_t cap = x.q, m = x.m, k = st ? st[6] : 0;
+	const uint64_t expected = m > 0 ? seeds / m : 0;
+	fprintf(stderr,
+	        "correcting: %s, |C|=%llu |F|=%llu m=%llu k=%llu\n"
+	        "  checkpoint gap=%llu bytes, expected fill ~%llu (~%llu%% table occupancy)\n"
+	        "  table memory ~%llu MB\n",
+	        "hash table", (unsigned long long)cap, (unsigned long long)x.f_size, (unsigned long long)m,
+	        (unsigned long long)k, (unsigned long long)m, (unsigned long long)expected,
+	        (unsigned long long)(cap > 0 ? expected * 100 / cap : 0), (unsigned long long)(cap * 24 / 1048576));
+	const uint64_t passed = st ? st[0] : 0, stored = st ? st[1] : 0, in_cap = st ? st[7] : 0;
+	fprintf(stderr,
+	        "  build: %llu seeds, %llu passed checkpoint (%.2f%%), %llu stored, %llu collisions\n"
+	        "  build: table occupancy %llu/%llu (%.1f%%)\n",
+	        (unsigned long long)seeds, (unsigned long long)passed, seeds > 0 ? (double)passed / seeds * 100.0 : 0.0,
+	        (unsigned long long)stored, (unsigned long long)(in_cap - stored), (unsigned long long)stored,
+	        (unsigned long long)cap, cap > 0 ? (double)stored / cap * 100.0 : 0.0);
+	const uint64_t vseeds = d.v_len >= p ? d.v_len - p + 1 : 0;
+	const uint64_t ck = st ? st[2] : 0, fpm = st ? st[3] : 0, bm = st ? st[4] : 0, mt = st ? st[5] : 0;
+	fprintf(stderr,
+	        "  scan: %llu V positions, %llu checkpoints (%.3f%%), %llu matches\n"
+	        "  scan: hit rate %.1f%% (of checkpoints), fp collisions %llu, byte mismatches %llu\n",
+	        (unsigned long long)vseeds, (unsigned long long)ck, vseeds > 0 ? (double)ck / vseeds * 100.0 : 0.0,
+	        (unsigned long long)mt, ck > 0 ? (double)mt / ck * 100.0 : 0.0, (unsigned long long)fpm,
+	        (unsigned long long)bm);
+	print_command_stats(cmds);
+}
 
 extern "C" {
 
@@ -626,6 +743,12 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t* P) { return P ? P->out_bound : 0; }
 uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t* P) { return P ? P->n : 0; }
 uint32_t dg_encode_plan_flags(const dg_encode_plan_t* P) { return P && P->members ? DG_PLAN_MEMBERS : 0u; }
+
+int dg_encode_plan_set_stats(dg_encode_plan_t* P, uint64_t* d_stats) {
+	if (!P) return DG_ERR_INVALID_ARG;
+	P->stats = d_stats;
+	return DG_OK;
+}
 #ifdef DG_AB_SWITCHES
 // A/B and profiling builds only: the member kernel's outputs of the last run
 // (device pointers; scripts/member_debug.py)
@@ -759,6 +882,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.table_tags = P->d_tags.as<uint32_t>();
 		a.buf_cap = (uint32_t)P->opts.buf_cap;
 		a.dbg = P->dbg;
+		a.stats = P->algo == DG_ALGO_CORRECTING ? P->stats : nullptr;
 		if (P->algo == DG_ALGO_ONEPASS) {
 			if (P->fused) {
 				a.out = d_out;

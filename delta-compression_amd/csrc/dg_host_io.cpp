@@ -86,8 +86,18 @@ int dg_encode_batch(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* const
 	if (rc) return rc;
 	const uint64_t bound = dg_encode_plan_output_bound(plan);
 
+	const bool verbose = opts && ((opts->flags >> DG_OPT_VERBOSE) & 1);
 	Pinned h_in, h_off, h_st;
-	Dev d_ref, d_ver, d_out, d_off, d_st;
+	Dev d_ref, d_ver, d_out, d_off, d_st, d_stats;
+	std::vector<uint64_t> stats;
+	if (verbose) {   // the reference's diagnostics (dg_encode_plan_set_stats)
+		if (!d_stats.alloc(64ull * n) || hipMemsetAsync(d_stats.p, 0, 64ull * n, st) != hipSuccess) {
+			dg_encode_plan_destroy(plan);
+			return DG_ERR_NOMEM;
+		}
+		dg_encode_plan_set_stats(plan, d_stats.as<uint64_t>());
+		stats.assign(8ull * n, 0);
+	}
 	rc = DG_ERR_NOMEM;
 	if (!h_in.alloc(rt + vt) || !h_off.alloc(8ull * (n + 1)) || !h_st.alloc(4ull * n) ||
 	    !d_ref.alloc(rt) || !d_ver.alloc(vt) || !d_out.alloc(bound) ||
@@ -121,10 +131,15 @@ int dg_encode_batch(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* const
 	Pinned h_out;
 	if (!h_out.alloc(total) ||
 	    hipMemcpyAsync(h_out.p, d_out.p, total, hipMemcpyDeviceToHost, st) != hipSuccess ||
+	    (verbose && hipMemcpyAsync(stats.data(), d_stats.p, 64ull * n, hipMemcpyDeviceToHost, st) != hipSuccess) ||
 	    hipStreamSynchronize(st) != hipSuccess) {
 		dg_encode_plan_destroy(plan);
 		return DG_ERR_HIP;
 	}
+	if (verbose)
+		for (uint32_t i = 0; i < n; ++i)
+			if (h_st.as<int32_t>()[i] == DG_OK)
+				dg::print_verbose(plan, i, stats.data() + 8ull * i, h_out.as<uint8_t>() + off[i], off[i + 1] - off[i]);
 	dg_encode_plan_destroy(plan);
 	int first_bad = DG_OK;
 	for (uint32_t i = 0; i < n; ++i) {

@@ -192,6 +192,15 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
                                const char **names, int n);
+/* --verbose counters (correcting plans): d_stats = 8 u64 per pair in device
+ * memory, zeroed by the caller (NULL = off, the default): seeds passing the
+ * build's checkpoint test, slots stored, scan checkpoints, fingerprint
+ * mismatches, byte mismatches, matches, the checkpoint class k, passing
+ * seeds whose slot is inside the table (the dbg_* counters of
+ * correcting.c:95-98).  dg_encode / dg_encode_batch with DG_OPT_VERBOSE set
+ * print the reference's diagnostic lines to stderr from these and the delta
+ * (onepass.c:64-69, 277-285; correcting.c:137-152, 200-214, 470-485). */
+int dg_encode_plan_set_stats(dg_encode_plan_t *plan, uint64_t *d_stats);
 /* How the plan runs (bit flags): DG_PLAN_MEMBERS = onepass through verified
  * diagonal members (DG_LIMIT_ONEPASS_MEMBERS). */
 #define DG_PLAN_MEMBERS 1u
