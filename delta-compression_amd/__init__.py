@@ -12,6 +12,10 @@ Names and argument meanings follow the reference's interface for this path:
 * ``crc64_xz(data)``                — ``delta_crc64_xz`` (src/c/delta.h:294).
 * ``decode(R, delta)``              — ``delta decode`` (main.c:323-400).
 * ``info(delta)``                   — ``delta info`` (main.c:402-425).
+* ``diff`` / ``diff_onepass`` / ``diff_correcting``, ``place_commands``,
+  ``unplace_commands``, ``encode_delta``, ``decode_delta`` — the command-list
+  level of src/python/delta.py:376-999 (the differencing on the GPU, the
+  container walk in the library's host code).
 
 Everything runs on the GPU.  Importing this package without the built
 library, or calling it without a visible GPU, raises — there is no CPU
@@ -27,7 +31,11 @@ from ._lib import (  # noqa: F401
     MAX_TABLE_SIZE,
     SEED_LEN,
     TABLE_SIZE,
+    AddCmd,
     Context,
+    CopyCmd,
+    PlacedAdd,
+    PlacedCopy,
     DeltaError,
     DiffOptions,
     EncodePlan,
@@ -40,14 +48,23 @@ from ._lib import (  # noqa: F401
     MEMBERS_ON,
     crc64_xz,
     decode,
+    decode_delta,
     default_context,
+    diff,
+    diff_correcting,
+    diff_onepass,
+    diff_placed,
     encode,
     encode_batch,
+    encode_delta,
     encode_pipelined,
     info,
     lib,
     make_inplace,
+    output_size,
+    place_commands,
     status_string,
+    unplace_commands,
 )
 
 __all__ = [
@@ -56,4 +73,6 @@ __all__ = [
     "crc64_xz", "decode", "default_context", "encode", "encode_batch", "encode_pipelined", "info", "lib",
     "make_inplace", "status_string", "LIB_PATH", "LIMIT_TABLE_POOL_BYTES",
     "LIMIT_ONEPASS_MEMBERS", "MEMBERS_AUTO", "MEMBERS_ON", "MEMBERS_OFF",
+    "CopyCmd", "AddCmd", "PlacedCopy", "PlacedAdd", "diff", "diff_onepass", "diff_correcting",
+    "diff_placed", "place_commands", "unplace_commands", "output_size", "encode_delta", "decode_delta",
 ]

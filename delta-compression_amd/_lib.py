@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -23,6 +24,7 @@ MAX_TABLE_SIZE = 1073741827
 BUF_CAP = 256
 OPT_VERBOSE, OPT_SPLAY, OPT_INPLACE, OPT_POLICY_CONSTANT = 0, 1, 2, 3
 POLICIES = {"localmin": 0, "constant": 1}
+CMD_COPY, CMD_ADD = 0, 1   # DG_CMD_COPY / DG_CMD_ADD
 
 _ALGOS = {"greedy": ALGO_GREEDY, "onepass": ALGO_ONEPASS, "correcting": ALGO_CORRECTING}
 
@@ -83,6 +85,15 @@ class DeltaInfo(C.Structure):
                 ("num_commands", C.c_uint64), ("num_copies", C.c_uint64),
                 ("num_adds", C.c_uint64), ("copy_bytes", C.c_uint64),
                 ("add_bytes", C.c_uint64)]
+
+
+class PlacedCommandC(C.Structure):   # dg_placed_command_t
+    _fields_ = [("tag", C.c_uint32), ("src", C.c_uint64), ("dst", C.c_uint64), ("length", C.c_uint64),
+                ("data", C.POINTER(C.c_uint8))]
+
+
+class Commands(C.Structure):         # dg_commands_t
+    _fields_ = [("data", C.POINTER(PlacedCommandC)), ("len", C.c_size_t), ("storage", C.c_void_p)]
 
 
 def _share_torch_runtime() -> None:
@@ -147,6 +158,11 @@ def _load() -> C.CDLL:
         "dg_decode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
         "dg_decode_plan_destroy": (None, [vp]),
         "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
+        "dg_diff": (C.c_int, [vp, C.c_int, u8p, sz, u8p, sz, C.POINTER(DiffOptions), C.POINTER(Commands)]),
+        "dg_delta_decode": (C.c_int, [u8p, sz, C.POINTER(Commands), C.POINTER(DeltaInfo)]),
+        "dg_encode_commands": (C.c_int, [C.POINTER(PlacedCommandC), sz, C.c_int, u64, C.c_uint8 * 8,
+                                         C.c_uint8 * 8, C.POINTER(Buffer)]),
+        "dg_commands_free": (None, [C.POINTER(Commands)]),
         "dg_make_inplace": (C.c_int, [u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer), C.POINTER(InplaceStats)]),
         "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
         "dg_synth_transpose_pairs_device": (C.c_int, [vp, u64, u32, u64, u32, C.POINTER(Pair),
@@ -481,3 +497,143 @@ def info(delta: bytes) -> dict:
         "num_commands": d.num_commands, "num_copies": d.num_copies, "num_adds": d.num_adds,
         "copy_bytes": d.copy_bytes, "add_bytes": d.add_bytes,
     }
+
+
+# ── command lists (src/python/delta.py:44-96, 854-1000; delta.h:94-137) ──────
+
+@dataclass
+class CopyCmd:
+    """Copy R[offset : offset+length] to the output (delta.py:44-51)."""
+    offset: int
+    length: int
+
+
+@dataclass
+class AddCmd:
+    """Append literal bytes (delta.py:54-62)."""
+    data: bytes
+
+
+@dataclass
+class PlacedCopy:
+    """COPY with explicit source and destination (delta.py:72-80)."""
+    src: int
+    dst: int
+    length: int
+
+
+@dataclass
+class PlacedAdd:
+    """ADD at an explicit destination (delta.py:83-92)."""
+    dst: int
+    data: bytes
+
+
+def _placed_list(cl: Commands) -> list:
+    out = []
+    for i in range(cl.len):
+        c = cl.data[i]
+        if c.tag == CMD_COPY:
+            out.append(PlacedCopy(c.src, c.dst, c.length))
+        else:
+            out.append(PlacedAdd(c.dst, C.string_at(c.data, c.length) if c.length else b""))
+    return out
+
+
+def diff(R: bytes, V: bytes, algorithm="onepass", p: int = SEED_LEN, q: int = TABLE_SIZE,
+         buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE, verbose: bool = False,
+         ctx: Optional[Context] = None) -> list:
+    """delta_diff / diff_onepass / diff_correcting (delta.py:376, 576): the
+    algorithm's commands (CopyCmd / AddCmd), computed by the GPU encoder
+    (dg_diff)."""
+    return unplace_commands(diff_placed(R, V, algorithm, p, q, buf_cap, max_table, verbose, ctx))
+
+
+def diff_placed(R: bytes, V: bytes, algorithm="onepass", p: int = SEED_LEN, q: int = TABLE_SIZE,
+                buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE, verbose: bool = False,
+                ctx: Optional[Context] = None) -> list:
+    """place_commands(diff(...)) in one call (dg_diff returns the placed form)."""
+    ctx = ctx or default_context()
+    cl = Commands()
+    o = _opts(p, q, buf_cap, max_table, verbose=verbose)
+    ctx.check(lib.dg_diff(ctx.handle, _algo(algorithm), _u8(R), len(R), _u8(V), len(V), C.byref(o),
+                          C.byref(cl)), "dg_diff")
+    try:
+        return _placed_list(cl)
+    finally:
+        lib.dg_commands_free(C.byref(cl))
+
+
+def diff_onepass(R: bytes, V: bytes, p: int = SEED_LEN, q: int = TABLE_SIZE, **kw) -> list:
+    return diff(R, V, "onepass", p=p, q=q, **kw)
+
+
+def diff_correcting(R: bytes, V: bytes, p: int = SEED_LEN, q: int = TABLE_SIZE,
+                    buf_cap: int = BUF_CAP, **kw) -> list:
+    return diff(R, V, "correcting", p=p, q=q, buf_cap=buf_cap, **kw)
+
+
+def output_size(commands: list) -> int:
+    """delta.py:848-851."""
+    return sum(c.length if isinstance(c, CopyCmd) else len(c.data) for c in commands)
+
+
+def place_commands(commands: list) -> list:
+    """Sequential destinations (delta.py:854-865, apply.c:136-164)."""
+    out, dst = [], 0
+    for c in commands:
+        if isinstance(c, CopyCmd):
+            out.append(PlacedCopy(c.offset, dst, c.length))
+            dst += c.length
+        else:
+            out.append(PlacedAdd(dst, bytes(c.data)))
+            dst += len(c.data)
+    return out
+
+
+def unplace_commands(placed: list) -> list:
+    """Placed -> algorithm commands in destination order, stable
+    (delta.py:868-895, apply.c:168-225)."""
+    order = sorted(range(len(placed)), key=lambda i: placed[i].dst)
+    return [CopyCmd(placed[i].src, placed[i].length) if isinstance(placed[i], PlacedCopy)
+            else AddCmd(placed[i].data) for i in order]
+
+
+def encode_delta(commands: list, *, inplace: bool = False, version_size: int, src_crc: bytes,
+                 dst_crc: bytes) -> bytes:
+    """Placed commands -> DLT\\x03 bytes (delta.py:939-964) via dg_encode_commands."""
+    if len(src_crc) != 8 or len(dst_crc) != 8:
+        raise ValueError("src_crc and dst_crc must be 8 bytes")
+    n = len(commands)
+    arr = (PlacedCommandC * max(n, 1))()
+    keep = []
+    for i, c in enumerate(commands):
+        if isinstance(c, PlacedCopy):
+            arr[i] = PlacedCommandC(CMD_COPY, c.src, c.dst, c.length, None)
+        else:
+            b = bytes(c.data)
+            keep.append(b)
+            arr[i] = PlacedCommandC(CMD_ADD, 0, c.dst, len(b), _u8(b))
+    out = Buffer()
+    rc = lib.dg_encode_commands(arr, n, int(inplace), version_size, (C.c_uint8 * 8)(*src_crc),
+                                (C.c_uint8 * 8)(*dst_crc), C.byref(out))
+    if rc:
+        raise DeltaError(rc, "dg_encode_commands")
+    try:
+        return C.string_at(out.data, out.len)
+    finally:
+        lib.dg_buffer_free(C.byref(out))
+
+
+def decode_delta(data: bytes):
+    """delta.py:967-999: (commands, inplace, version_size, src_crc, dst_crc)
+    via dg_delta_decode; a malformed stream raises DeltaError (code 8)."""
+    cl, hdr = Commands(), DeltaInfo()
+    rc = lib.dg_delta_decode(_u8(data), len(data), C.byref(cl), C.byref(hdr))
+    if rc:
+        raise DeltaError(rc, "dg_delta_decode")
+    try:
+        return (_placed_list(cl), bool(hdr.inplace), hdr.version_size, bytes(hdr.src_crc),
+                bytes(hdr.dst_crc))
+    finally:
+        lib.dg_commands_free(C.byref(cl))

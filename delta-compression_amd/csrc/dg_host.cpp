@@ -154,12 +154,6 @@ void dg_diff_options_default(dg_diff_options_t* o) {
 	o->flags = 0;
 }
 
-void dg_buffer_free(dg_buffer_t* b) {
-	if (!b) return;
-	free(b->data);
-	b->data = nullptr;
-	b->len = 0;
-}
 
 const char* dg_status_string(int s) {
 	switch (s) {

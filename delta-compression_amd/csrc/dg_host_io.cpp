@@ -419,6 +419,24 @@ int dg_encode(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* r, size_t r
 	return rc ? rc : st;
 }
 
+int dg_diff(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* r, size_t r_len, const uint8_t* v,
+            size_t v_len, const dg_diff_options_t* opts, dg_commands_t* out) {
+	// delta_diff + delta_place_commands (delta.h:280-284, apply.c:136-164):
+	// the device encodes, the host lists the commands of the standard delta,
+	// which holds them 1:1 in algorithm order (encoding.c:69-83)
+	if (!out || !opts) return DG_ERR_INVALID_ARG;
+	out->data = nullptr;
+	out->len = 0;
+	out->storage = nullptr;
+	dg_diff_options_t o = *opts;
+	o.flags &= ~(1ull << DG_OPT_INPLACE);
+	dg_buffer_t d{nullptr, 0};
+	int rc = dg_encode(ctx, algo, r, r_len, v, v_len, &o, &d);
+	if (rc == DG_OK) rc = dg_delta_decode(d.data, d.len, out, nullptr);
+	dg_buffer_free(&d);
+	return rc;
+}
+
 int dg_crc64_xz_batch_device(dg_context_t* ctx, const uint8_t* d_arena, const dg_span_t* spans,
                              uint32_t n, uint64_t* d_crc, void* stream);
 
@@ -437,40 +455,6 @@ int dg_crc64_xz(dg_context_t* ctx, const uint8_t* data, size_t len, uint8_t out[
 		return DG_ERR_HIP;
 	const uint64_t v = *h.as<uint64_t>();
 	for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(v >> (56 - 8 * i));
-	return DG_OK;
-}
-
-int dg_delta_info(const uint8_t* d, size_t len, dg_delta_info_t* info) {
-	// src/c/encoding.c:111-178 walk, summary as delta_placed_summary (apply.c:98-115)
-	if (!d || !info) return DG_ERR_INVALID_ARG;
-	memset(info, 0, sizeof *info);
-	if (len < DG_HEADER_SIZE || memcmp(d, "DLT\x03", 4) != 0) return DG_ERR_MALFORMED;
-	info->inplace = d[4] & 1;
-	info->version_size = rd_u32be(d + 5);
-	memcpy(info->src_crc, d + 9, 8);
-	memcpy(info->dst_crc, d + 17, 8);
-	size_t pos = DG_HEADER_SIZE;
-	while (pos < len) {
-		const uint8_t t = d[pos++];
-		if (t == 0) return DG_OK;
-		if (t == 1) {
-			if (pos + 12 > len) return DG_ERR_MALFORMED;
-			info->num_copies++;
-			info->copy_bytes += rd_u32be(d + pos + 8);
-			pos += 12;
-		} else if (t == 2) {
-			if (pos + 8 > len) return DG_ERR_MALFORMED;
-			const uint32_t l = rd_u32be(d + pos + 4);
-			pos += 8;
-			if (pos + l > len) return DG_ERR_MALFORMED;
-			info->num_adds++;
-			info->add_bytes += l;
-			pos += l;
-		} else {
-			return DG_ERR_MALFORMED;
-		}
-		info->num_commands++;
-	}
 	return DG_OK;
 }
 
@@ -591,10 +575,8 @@ extern "C" int dg_decode(dg_context_t* ctx, const uint8_t* r, size_t r_len, cons
 	if (!ctx || !out || (r_len && !r) || (delta_len && !delta)) return DG_ERR_INVALID_ARG;
 	out->data = nullptr;
 	out->len = 0;
-	dg_delta_info_t inf;
 	if (delta_len < DG_HEADER_SIZE || memcmp(delta, "DLT\x03", 4) != 0) return DG_ERR_MALFORMED;
 	const uint64_t vsize = rd_u32be(delta + 5);
-	(void)inf;
 	const uint64_t cap = std::max<uint64_t>(vsize, r_len);
 	hipStream_t st = (hipStream_t)dg_context_stream(ctx);
 	Dev d_r, d_d, d_o, d_len, d_st;

@@ -331,6 +331,52 @@ typedef struct {
 
 int dg_delta_info(const uint8_t *delta, size_t len, dg_delta_info_t *info);
 
+/* ── command lists (delta.h:94-137, 280-284, 326-368) ───────────────────
+ *
+ * For callers that work between the algorithm and the container, as in
+ * HOWTO.md:426-464 (delta_diff -> delta_place_commands -> delta_encode;
+ * delta_decode -> delta_apply_placed).  One record type serves both the
+ * algorithm's commands (delta_command_t: COPY offset = src, ADD data) and the
+ * placed ones (delta_placed_command_t: + dst).  Lengths and offsets are in
+ * bytes; ADD data point into storage owned by the list. */
+#define DG_CMD_COPY 0   /* == CMD_COPY, PCMD_COPY */
+#define DG_CMD_ADD  1   /* == CMD_ADD, PCMD_ADD */
+typedef struct {
+	uint32_t       tag;      /* DG_CMD_COPY or DG_CMD_ADD */
+	uint64_t       src;      /* COPY: offset in R (0 for ADD) */
+	uint64_t       dst;      /* offset in V */
+	uint64_t       length;
+	const uint8_t *data;     /* ADD: `length` literal bytes (NULL for COPY) */
+} dg_placed_command_t;
+typedef struct {
+	dg_placed_command_t *data;
+	size_t               len;
+	void                *storage;   /* owns data and the ADD bytes */
+} dg_commands_t;
+void dg_commands_free(dg_commands_t *cmds);
+
+/* delta_diff(algo, R, V, opts) followed by delta_place_commands (apply.c:
+ * 136-164): the commands of the delta dg_encode produces, in algorithm order
+ * with sequential dst (so dropping dst gives delta_diff's list).  Runs on the
+ * GPU; DG_OPT_INPLACE in opts->flags is ignored (in-place conversion is
+ * dg_make_inplace on an encoded delta). */
+int dg_diff(dg_context_t *ctx, dg_algorithm_t algo,
+            const uint8_t *r, size_t r_len, const uint8_t *v, size_t v_len,
+            const dg_diff_options_t *opts, dg_commands_t *out);
+/* delta_decode (encoding.c:111-178): the placed commands of a delta in stream
+ * order, and its header (hdr may be NULL; it receives dg_delta_info's
+ * summary).  DG_ERR_MALFORMED where the reference exits with "not a delta
+ * file" / "truncated ..." / "unknown command type".  Host only. */
+int dg_delta_decode(const uint8_t *delta, size_t len, dg_commands_t *out,
+                    dg_delta_info_t *hdr);
+/* delta_encode (encoding.c:39-90): placed commands -> DLT\x03 bytes,
+ * out->data malloc'd.  Offsets, lengths and version_size of 4 GiB or more
+ * (which the format's u32 fields cannot hold) give DG_ERR_INVALID_ARG.  Host
+ * only. */
+int dg_encode_commands(const dg_placed_command_t *cmds, size_t n, int inplace,
+                       uint64_t version_size, const uint8_t src_crc[DG_CRC_SIZE],
+                       const uint8_t dst_crc[DG_CRC_SIZE], dg_buffer_t *out);
+
 /* ── in-place conversion (host; src/c/inplace.c:272-736) ───────────────────
  *
  * Converts a standard delta against R into an in-place delta: the chain of
