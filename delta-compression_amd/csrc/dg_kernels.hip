@@ -879,6 +879,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	__shared__ uint16_t cmds[kDecMaxCmds];
 	__shared__ uint16_t jumps[kDecMaxCmds / 8 + 1];
 	__shared__ uint32_t sh[8];   // walk results and window flags
+	__shared__ uint32_t bsum[2 * (kDecMaxCmds / 64 + 1)];   // per batch: first written dst, max end
 	uint16_t* N2 = NX;
 	uint16_t* N4 = NX + kDecWin;
 	uint16_t* N8 = NX + 2 * kDecWin;
@@ -1088,22 +1089,37 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 				if (c.dst + c.len > bsz) bad = true;
 				if (c.kind == 1 && c.src + c.len > (inplace ? bsz : rl)) bad = true;
 			}
-			// order-free: destinations increasing and disjoint (< 2^32: bsz
-			// checked) and no in-place COPY that moves
-			const uint32_t end32 = (uint32_t)(c.dst + c.len), dst32 = (uint32_t)c.dst;
-			uint32_t prev_end = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)end32, 0x138, 0xF, 0xF, false);
-			if (lane == 0 && b > 0) {   // the last command of the batch before
-				const DecCmd p = dec_cmd(w, cmds, 64 * b - 1, cnt, pos);
-				prev_end = (uint32_t)(p.dst + p.len);
-			}
-			const bool unordered = c.mine && (lane > 0 || b > 0) && dst32 < prev_end;
+			// order-free: the commands that write (an in-place COPY with src ==
+			// dst writes nothing: apply.c:257-266 memmoves a range onto itself,
+			// and the in-place format puts the ADDs after the COPYs,
+			// inplace.c:711-725) have increasing, disjoint destinations (< 2^32:
+			// bsz checked), and no in-place COPY moves.  Within the batch by a
+			// prefix max of the write ends; across batches by the summaries.
+			const bool writes = c.mine && c.len != 0 && !(inplace && c.kind == 1 && c.src == c.dst);
+			const uint32_t end32 = writes ? (uint32_t)(c.dst + c.len) : 0u, dst32 = (uint32_t)c.dst;
+			const uint32_t incl_end = wave_incl_max(end32);
+			const bool unordered = writes && dst32 < wave_shr1z(incl_end);
 			const bool moves = c.mine && inplace && c.kind == 1 && c.src != c.dst;
+			const uint64_t wm = __ballot(writes);
+			const uint32_t first_dst = wm ? rdlane(dst32, ffs64(wm)) : ~0u;
+			if (lane == 0) {
+				bsum[2 * b] = first_dst;
+				bsum[2 * b + 1] = rdlane(incl_end, 63);
+			}
 			if (__ballot(bad) && lane == 0) atomicOr(&sh[4], 1u);
 			if (__ballot(unordered || moves) && lane == 0) atomicOr(&sh[5], 1u);
 		}
 		__syncthreads();
 		if (sh[4]) st = 8;
-		const bool free_win = !sh[5];
+		bool cross = false;   // a batch writes below the end of an earlier batch's writes
+		for (uint32_t b = 0, run = 0; b < nb; ++b) {
+			const uint32_t f = bsum[2 * b], e = bsum[2 * b + 1];
+			if (f != ~0u) {
+				cross = cross || f < run;
+				run = umax32(run, e);
+			}
+		}
+		const bool free_win = !sh[5] && !cross;
 		if (!free_win) DPROF_INC(DP_ORDERED);
 		DPROF_ADD(DP_HDR, th0);
 		DPROF_T(tc0);

@@ -21,6 +21,7 @@ NAMES = ["fill", "win_load", "n1", "doubling", "walk", "expand", "hdr+checks", "
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=1024)
+    ap.add_argument("--inplace", action="store_true", help="C5: convert with make_inplace(localmin)")
     args = ap.parse_args()
     os.environ.setdefault("DG_LIB_VARIANT", "prof")
     import torch
@@ -44,6 +45,14 @@ def main():
             est.data_ptr(), None)
     torch.cuda.synchronize()
     o = offs.cpu().tolist()
+    if args.inplace:   # the C5 workload (bench.py bench_decode)
+        std = d_arena[:o[-1]].cpu().numpy().tobytes()
+        ref_h = ref.cpu().numpy().tobytes()
+        ds = [dg.make_inplace(ref_h[i * L:(i + 1) * L], std[o[i]:o[i + 1]], policy="localmin") for i in range(n)]
+        o = [0]
+        for d in ds:
+            o.append(o[-1] + len(d))
+        d_arena = torch.frombuffer(bytearray(b"".join(ds)), dtype=torch.uint8).to("cuda")
     plan = dg.DecodePlan(ctx, [(r, rl, o[i], o[i + 1] - o[i], v, vl) for i, (r, rl, v, vl) in enumerate(layout)])
     out = torch.empty_like(ver)
     olen = torch.empty(n, dtype=torch.int64, device="cuda")
