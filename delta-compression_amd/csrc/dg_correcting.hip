@@ -49,9 +49,31 @@ __device__ __forceinline__ uint64_t fold61c(uint64_t lo, uint64_t hi) {
 	return mod_m61(lo + ((hi & ((1ULL << 29) - 1)) << 32) + (hi >> 29));
 }
 
+// One rolling step (hash.c:62-98) fp' = (fp - out 263^(p-1)) 263 + in
+// = fp 263 + nb + in (mod M), with nb = -out 263^p mod M from a table
+// (roll_table): with fp = h 2^32 + l (h < 2^29),
+//   fp 263 + nb + in = (l 263 + nb_lo + in) + (h 263 + nb_hi) 2^32
+// and (h 263 + nb_hi) 2^32 == (.. >> 29) + (.. & (2^29-1)) 2^32, so the sum
+// is < 2^62 and one fold plus one subtract make it canonical.  Two 32x32
+// multiply-adds instead of the subtract-fold-multiply-fold of the textbook
+// form.  fp must be canonical (< M); so is the result.
+__device__ __forceinline__ uint64_t roll61(uint64_t fp, uint64_t nb, uint32_t in) {
+	const uint64_t plo = (uint64_t)(uint32_t)fp * (uint32_t)kBase + (uint32_t)nb + in;   // < 2^42
+	const uint64_t phi = (uint64_t)(uint32_t)(fp >> 32) * (uint32_t)kBase + (nb >> 32);  // < 2^39
+	const uint64_t t = plo + ((phi & ((1ULL << 29) - 1)) << 32) + (phi >> 29);           // < 2^61 + 2^43
+	const uint64_t r = (t & kMersenne) + (t >> 61);
+	return r >= kMersenne ? r - kMersenne : r;
+}
+
 // x * c mod M for x < 2^61 and c < 2^32
 __device__ __forceinline__ uint64_t mulsmall61(uint64_t x, uint32_t c) {
 	return fold61c((x & 0xFFFFFFFFull) * c, (x >> 32) * c);
+}
+
+// the roll61 table entry of byte x: -x 263^p mod M (c = 263^(p-1) mod M)
+__device__ __forceinline__ uint64_t roll_table(uint32_t x, uint64_t c) {
+	const uint64_t v = mulsmall61(mulsmall61(c, (uint32_t)kBase), x);   // x 263^p
+	return v ? kMersenne - v : 0;
 }
 
 // checkpoint class k: fingerprint of V[|V|/2 .. +p) (correcting.c:131-136),
@@ -247,7 +269,7 @@ __global__ __launch_bounds__(256) void correcting_stats_kernel(EncodeArgs a) {
 
 __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArgs a, uint32_t nchunk,
                                                                        uint32_t lds_cap) {
-	__shared__ uint64_t ob[256];   // x * 263^(p-1) mod M: the byte leaving the window
+	__shared__ uint64_t nb[256];   // roll61 table: -x 263^p mod M for the byte leaving the window
 	const uint32_t xcd = blockIdx.x & 7u, i = blockIdx.x >> 3;
 	const uint32_t pair = (i / nchunk) * 8u + xcd, chunk = i % nchunk;
 	if (pair >= a.n_pairs) return;
@@ -260,10 +282,7 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 	if (blk0 >= seeds || pd.v_len == 0) return;
 	const uint8_t* R = a.ref + pd.r_off;
 	const uint64_t top = a.powc[0];
-	{
-		const uint32_t x = threadIdx.x;
-		ob[x] = fold61c((uint64_t)x * (uint32_t)top, (uint64_t)x * (uint32_t)(top >> 32));
-	}
+	nb[threadIdx.x] = roll_table(threadIdx.x, top);
 	__syncthreads();
 	const uint64_t k = a.kcls[pair];
 	uint32_t* H = a.ctab + pp.tab_base;
@@ -293,8 +312,7 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 #pragma unroll
 		for (uint32_t j = 0; j < kBuildSeedsPerLane; ++j) {
 			if (j) {   // roll (hash.c:62-98)
-				const uint64_t t = mod_m61(fp + kMersenne - ob[byte_at(j - 1)]);
-				fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 15), (t >> 32) * (uint32_t)kBase);
+				fp = roll61(fp, nb[byte_at(j - 1)], byte_at(j + 15));
 			}
 			uint32_t slot;
 			if (passes(fp, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
@@ -305,8 +323,7 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 	for (uint32_t j = 0; j < cnt; ++j) {
 		if (j) {   // roll: (fp - R[a-1] * 263^(p-1)) * 263 + R[a-1+p]   (hash.c:62-98)
 			const uint64_t s = s0 + j;
-			const uint64_t t = mod_m61(fp + kMersenne - ob[R[s - 1]]);
-			fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + R[s - 1 + p], (t >> 32) * (uint32_t)kBase);
+			fp = roll61(fp, nb[R[s - 1]], R[s - 1 + p]);
 		}
 		uint32_t slot;
 		if (passes(fp, &slot)) atomicMin(&H[slot], (uint32_t)(s0 + j));
@@ -322,7 +339,7 @@ constexpr uint32_t kBuildLdsBlock = 1024;
 
 __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(EncodeArgs a, uint32_t lds_cap) {
 	extern __shared__ uint32_t T[];
-	__shared__ uint64_t ob[256];
+	__shared__ uint64_t nb[256];   // roll61 table
 	const uint32_t pair = blockIdx.x;
 	const uint32_t tid = threadIdx.x;
 	const PairPlanDev pp = a.pplan[pair];
@@ -331,10 +348,7 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 	const uint32_t cap = (uint32_t)pp.q;
 	uint32_t* H = a.ctab + pp.tab_base;
 	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) T[i] = kNone;
-	if (tid < 256) {
-		const uint64_t top = a.powc[0];
-		ob[tid] = fold61c((uint64_t)tid * (uint32_t)top, (uint64_t)tid * (uint32_t)(top >> 32));
-	}
+	if (tid < 256) nb[tid] = roll_table(tid, a.powc[0]);
 	__syncthreads();
 	const uint32_t p = a.p;
 	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
@@ -379,10 +393,8 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 #pragma unroll
 					for (uint32_t j = 0; j < kBuildSeedsPerLane / 2; ++j) {
 						if (j) {   // roll (hash.c:62-98)
-							const uint64_t ta = mod_m61(fa + kMersenne - ob[byte_at(j - 1)]);
-							const uint64_t tb = mod_m61(fb + kMersenne - ob[byte_at(j + 15)]);
-							fa = fold61c((ta & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 15), (ta >> 32) * (uint32_t)kBase);
-							fb = fold61c((tb & 0xFFFFFFFFull) * (uint32_t)kBase + byte_at(j + 31), (tb >> 32) * (uint32_t)kBase);
+							fa = roll61(fa, nb[byte_at(j - 1)], byte_at(j + 15));
+							fb = roll61(fb, nb[byte_at(j + 15)], byte_at(j + 31));
 						}
 						insert(fa, (uint32_t)(s0 + j));
 						insert(fb, (uint32_t)(s0 + 16 + j));
@@ -392,8 +404,7 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 					for (uint32_t j = 0; j < cnt; ++j) {
 						if (j) {
 							const uint64_t s = s0 + j;
-							const uint64_t t = mod_m61(fp + kMersenne - ob[R[s - 1]]);
-							fp = fold61c((t & 0xFFFFFFFFull) * (uint32_t)kBase + R[s - 1 + p], (t >> 32) * (uint32_t)kBase);
+							fp = roll61(fp, nb[R[s - 1]], R[s - 1 + p]);
 						}
 						insert(fp, (uint32_t)(s0 + j));
 					}
