@@ -221,6 +221,76 @@ __device__ __forceinline__ bool long_member_ok(const uint8_t* SV, const uint8_t*
 	return !d2;
 }
 
+// long_member_ok for a member of exactly K rows (64 (K - 1) <= T < 64 K):
+// the row count is a compile-time constant, so none of the per-row uniform
+// predicates remain (88 % of C3's long members have K = 2, 11 % K = 3).
+template <uint32_t W, uint32_t K>
+__device__ __forceinline__ bool long_member_rows(const uint8_t* SV, const uint8_t* SR, uint32_t s0, uint32_t tl,
+                                                 uint32_t* filt, const ModQ& mq, uint64_t q, uint64_t qmag,
+                                                 uint32_t& pw) {
+	const uint32_t lane = lane_id();
+	constexpr uint32_t CT = K - 1;
+	const uint32_t LT = tl % 64;
+	VFilter<W> fl{filt};
+	uint32_t hsV[K], hfV[K], hfR[K];   // V slots, V / R window hashes
+	lds_order();
+	fl.clear();
+	lds_order();
+#pragma unroll
+	for (uint32_t cc = 0; cc < K; ++cc) {
+		hsV[cc] = kSentinel;
+		hfV[cc] = 0u;
+		hfR[cc] = 1u;
+		const uint32_t t = 64 * cc + lane;
+		if (cc < CT || t <= tl) {
+			const uint4 wv = lds16(SV, s0 + t), wr = lds16(SR, s0 + t);
+			hsV[cc] = slot_of(fp16_dot(wv.x, wv.y, wv.z, wv.w), mq, q, qmag);
+			hfV[cc] = win_hash(wv);
+			hfR[cc] = win_hash(wr);
+			if (cc == 0) pw = wv.x;
+			if (t != tl) fl.add(hfV[cc]);
+		}
+	}
+	pw = rdlane(pw, 0);
+	lds_order();
+	// (A) through T: V(c) == V(T) or R(l) == R(T) for a step before T
+	const uint32_t hT = rdlane(hfV[CT], LT), vT = rdlane(hsV[CT], LT);
+	bool bad = false;
+#pragma unroll
+	for (uint32_t c2 = 0; c2 < K; ++c2)
+		bad = bad || (__ballot(hfV[c2] == hT || hfR[c2] == hT) & (c2 < CT ? ~0ull : lanes_range(0, LT))) != 0;
+	// (A) off T: flagged steps' R hashes against every other step's V hash
+#pragma unroll
+	for (uint32_t cc = 0; cc < K; ++cc) {
+		const uint32_t t = 64 * cc + lane;
+		for (uint64_t w = __ballot(t < tl && fl.has(hfR[cc])); w && !bad; w &= w - 1) {
+			const uint32_t Lx = ffs64(w);
+			const uint32_t fR = rdlane(hfR[cc], Lx);
+#pragma unroll
+			for (uint32_t c2 = 0; c2 < K; ++c2) {
+				const bool other = 64 * c2 + lane <= tl && !(c2 == cc && lane == Lx);
+				if (__ballot(other && hfV[c2] == fR)) bad = true;
+			}
+		}
+	}
+	if (bad) return false;
+	// (B): the T step's V slot against the earlier V slots; R slots only when
+	// it repeats
+	bool d1 = false;
+#pragma unroll
+	for (uint32_t c2 = 0; c2 < K; ++c2)
+		d1 = d1 || (__ballot(hsV[c2] == vT) & (c2 < CT ? ~0ull : lanes_range(0, LT))) != 0;
+	if (!d1) return true;
+	const uint32_t rT = slot_lds(SR, s0 + tl, mq, q, qmag);
+	bool d2 = false;
+	for (uint32_t c2 = 0; c2 <= CT; ++c2) {
+		const uint32_t t2 = 64 * c2 + lane;
+		const uint32_t sr2 = t2 < tl ? slot_lds(SR, s0 + t2, mq, q, qmag) : kSentinel;
+		d2 = d2 || __ballot(t2 < tl && sr2 == rT) != 0;
+	}
+	return !d2;
+}
+
 // the staged region of one chunk in VGPRs (16 bytes per lane per row), loaded
 // while the previous chunk is verified
 constexpr uint32_t kStageRows = (kStage + 1023) / 1024;   // rows of 64 x 16 B (the last one partial)
@@ -525,7 +595,9 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			const uint32_t M = ffs64(LM);
 			const uint32_t s0 = rdlane(s, M), tl = rdlane(T, M), sn0 = rdlane(sn, M);
 			uint32_t pw;
-			const bool ok = long_member_ok<64>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw);
+			const bool ok = tl < 128 ? long_member_rows<64, 2>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw)
+			                : tl < 192 ? long_member_rows<64, 3>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw)
+			                           : long_member_ok<64>(SV, SR, s0, tl, L.filt, mq, q, qmag, pw);
 			if (lane == 0) {
 				*(uint4*)(srec + 4 * M) = make_uint4((uint32_t)(g0 + (int64_t)(s0 + tl)), sn0 - (s0 + tl), pw,
 				                                     ok ? 1u : 0u);
