@@ -547,26 +547,27 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 				const bool hit = (__ballot(fVl == rdlane(fRl, Lx)) & others) != 0;
 				bad = bad || (hit && lane == Lx);
 			}
-			// T steps: (A) through T (a V or R repeat of the T window among the
-			// member's earlier steps), then (B) — the T step's V slot against
-			// the earlier V slots, R slots computed on demand
-			uint32_t sR = kSentinel - 1u;
-			bool have_sR = false;
-			for (uint64_t w = __ballot(isT); w; w &= w - 1) {
-				const uint32_t LT = ffs64(w);
-				const uint64_t before = lanes_range(rdlane(fb, LT), LT);
-				const uint32_t hT = rdlane(fVl, LT);
-				if ((__ballot(fVl == hT || fRl == hT) & before) != 0) {
-					bad = bad || lane == LT;
-					continue;
+			// T steps, all members at once: (A) through T (a V or R repeat of
+			// the T window among the member's earlier steps), then (B) — the T
+			// step's V slot against the earlier V slots, R slots only when one
+			// repeats.  Every step lane fetches its T step's values, the
+			// ballots flag the steps, and each T lane reads its member's bits.
+			{
+				const int tsel = (int)(((fb + mt_j) & 63u) << 2);   // this lane's T lane
+				const uint32_t hT = (uint32_t)__builtin_amdgcn_ds_bpermute(tsel, (int)fVl);
+				const uint32_t vT = (uint32_t)__builtin_amdgcn_ds_bpermute(tsel, (int)sV);
+				const bool step = live && !isT;
+				const uint64_t A1 = __ballot(step && (fVl == hT || fRl == hT));
+				const uint64_t B1 = __ballot(step && sV == vT);
+				bool badT = isT && (A1 & mem) != 0;
+				const bool d1 = isT && !badT && (B1 & mem) != 0;
+				if (__ballot(d1)) {   // rare: the R slots
+					const uint32_t sR = live ? slot_lds(SR, ms_j + t, mq, q, qmag) : kSentinel - 1u;
+					const uint32_t rT = (uint32_t)__builtin_amdgcn_ds_bpermute(tsel, (int)sR);
+					const uint64_t C1 = __ballot(step && sR == rT);
+					badT = badT || (d1 && (C1 & mem) != 0);
 				}
-				if ((__ballot(sV == rdlane(sV, LT)) & before) == 0) continue;
-				if (!have_sR) {
-					if (live) sR = slot_lds(SR, ms_j + t, mq, q, qmag);
-					have_sR = true;
-				}
-				const bool d2 = (__ballot(sR == rdlane(sR, LT)) & before) != 0;
-				bad = bad || (d2 && lane == LT);
+				bad = bad || badT;
 			}
 			// verdict at each member's T step; the record carries the ADD head
 			// (the first step's V window) and the COPY length
