@@ -714,6 +714,13 @@ struct DecCmd {
 	uint64_t src, dst, len;
 };
 
+// big-endian u32 at byte 1 + 4i of a 16-byte header image h[4] (i = 0, 1, 2)
+__device__ __forceinline__ uint32_t hdr_be32(const uint32_t (&h)[4], int i) {
+	return __builtin_bswap32(__builtin_amdgcn_alignbyte(h[i + 1], h[i], 1));
+}
+
+// The window holds >= 16 bytes past any command offset (win has 32 bytes of
+// slack), so a header is one unaligned 16-byte LDS read.
 template <typename WP>
 __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b, uint32_t cnt, uint64_t pos) {
 	DecCmd c{false, 0, 0, 0, 0};
@@ -721,15 +728,17 @@ __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b
 	c.mine = b + lane < cnt;
 	if (c.mine) {
 		const uint32_t cx = cmds[b + lane];
-		c.kind = w[cx];
+		uint32_t h[4];
+		__builtin_memcpy(h, w + cx, 16);
+		c.kind = h[0] & 0xFFu;
 		if (c.kind == 1) {
-			c.src = be32(w + cx + 1);
-			c.dst = be32(w + cx + 5);
-			c.len = be32(w + cx + 9);
+			c.src = hdr_be32(h, 0);
+			c.dst = hdr_be32(h, 1);
+			c.len = hdr_be32(h, 2);
 		} else {
 			c.src = pos + cx + 9;   // payload offset in the stream
-			c.dst = be32(w + cx + 1);
-			c.len = be32(w + cx + 5);
+			c.dst = hdr_be32(h, 0);
+			c.len = hdr_be32(h, 1);
 		}
 	}
 	return c;
@@ -873,7 +882,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	if (i >= a.n) return;
 	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
 	__shared__ __attribute__((aligned(16))) uint8_t win[kDecWin + 32];
-	__shared__ uint16_t N1[kDecWin];
+	__shared__ __attribute__((aligned(16))) uint16_t N1[kDecWin];
 	// N2, N4, N8 during the parse; the waves' flat-copy scratch afterwards
 	__shared__ __attribute__((aligned(16))) uint16_t NX[3 * kDecWin];
 	__shared__ uint16_t cmds[kDecMaxCmds];
@@ -977,45 +986,72 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		const uint8_t* w = win + shf;
 		DPROF_ADD(DP_LOAD, tl0);
 		DPROF_T(tn0);
-		// ── 2. N1: next command offset for a command starting at x ──
-		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
-			uint16_t nx = kNxBad;
-			if (x < avail) {
+		// ── 2. N1: next command offset for a command starting at x.  Thread
+		//    tid owns offsets [16 tid, 16 tid + 16): all default to malformed
+		//    (two 16-byte stores), and only offsets whose byte is a command
+		//    type (0, 1, 2: ~1.3 of 16 in a command stream) are decoded ──
+		static_assert(kDecWin == 16 * kDecBlock, "16 window offsets per thread");
+		{
+			const uint32_t x0 = 16 * tid;
+			constexpr uint32_t bb = (uint32_t)kNxBad | ((uint32_t)kNxBad << 16);
+			uint4* dst = reinterpret_cast<uint4*>(N1 + x0);
+			dst[0] = make_uint4(bb, bb, bb, bb);
+			dst[1] = make_uint4(bb, bb, bb, bb);
+			uint32_t d[4];
+			__builtin_memcpy(d, w + x0, 16);
+			uint32_t cand = 0;
+#pragma unroll
+			for (uint32_t k = 0; k < 16; ++k) cand |= (((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) <= 2u ? 1u : 0u) << k;
+			const uint32_t lim = avail > x0 ? umin32(avail - x0, 16u) : 0u;
+			cand &= (1u << lim) - 1u;
+			for (; cand; cand &= cand - 1) {
+				const uint32_t x = x0 + (uint32_t)__builtin_ctz(cand);
 				const uint32_t t = w[x];
-				if (t == 0) {
-					nx = kNxEnd;
-				} else if (t == 1 || t == 2) {
+				uint32_t nx = kNxEnd;
+				if (t != 0) {
 					const uint32_t hdr = t == 1 ? 13u : 9u;
 					if (x + hdr > avail) {
 						nx = pos + x + hdr > dl ? kNxBad : kNxCut;
 					} else {
-						const uint64_t len = t == 1 ? 0 : be32(w + x + 5);
+						uint32_t lw = 0;
+						__builtin_memcpy(&lw, w + x + 5, 4);
+						const uint64_t len = t == 1 ? 0 : __builtin_bswap32(lw);
 						const uint64_t end = (uint64_t)x + hdr + len;
 						if (pos + end > dl) nx = kNxBad;
-						else nx = end >= avail ? kNxFar : (uint16_t)end;
+						else nx = end >= avail ? kNxFar : (uint32_t)end;
 					}
 				}
+				N1[x] = (uint16_t)nx;
 			}
-			N1[x] = nx;
 		}
 		__syncthreads();
 		DPROF_ADD(DP_N1, tn0);
 		DPROF_T(td0);
 		// ── 3. pointer doubling ──
-		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
-			const uint16_t y = N1[x];
-			N2[x] = y >= kNxSpecial ? y : N1[y];
-		}
+		// (16 offsets per thread: two 16-byte reads, 16 independent gathers,
+		// two 16-byte stores)
+		auto dbl = [&](const uint16_t* src, uint16_t* dstN) {
+			const uint32_t x0 = 16 * tid;
+			const uint4* sp = reinterpret_cast<const uint4*>(src + x0);
+			const uint4 a = sp[0], b = sp[1];
+			const uint32_t in[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+			uint32_t o[8];
+#pragma unroll
+			for (uint32_t k = 0; k < 8; ++k) {
+				const uint32_t y0 = in[k] & 0xFFFFu, y1 = in[k] >> 16;
+				const uint32_t z0 = y0 >= kNxSpecial ? y0 : src[y0];
+				const uint32_t z1 = y1 >= kNxSpecial ? y1 : src[y1];
+				o[k] = z0 | (z1 << 16);
+			}
+			uint4* dp = reinterpret_cast<uint4*>(dstN + x0);
+			dp[0] = make_uint4(o[0], o[1], o[2], o[3]);
+			dp[1] = make_uint4(o[4], o[5], o[6], o[7]);
+		};
+		dbl(N1, N2);
 		__syncthreads();
-		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
-			const uint16_t y = N2[x];
-			N4[x] = y >= kNxSpecial ? y : N2[y];
-		}
+		dbl(N2, N4);
 		__syncthreads();
-		for (uint32_t x = tid; x < kDecWin; x += kDecBlock) {
-			const uint16_t y = N4[x];
-			N8[x] = y >= kNxSpecial ? y : N4[y];
-		}
+		dbl(N4, N8);
 		__syncthreads();
 		DPROF_ADD(DP_DBL, td0);
 		DPROF_T(tw0);
