@@ -185,7 +185,7 @@ struct CrcArgs {
 	const CrcSegDev* segs;
 	uint32_t n_segs;
 	uint32_t n_spans;
-	const uint64_t* tables;    // slice (8x256) + level nibble tables (6x256)
+	const uint64_t* tables;    // slice (8x256) + nibble tables: 6 levels, kseg, 16 pad inverses
 	uint64_t* seg_crc;
 	uint64_t* out;             // per span: CRC-64/XZ value
 	const uint64_t* xinv;      // 16 constants x^(-8t) mod P

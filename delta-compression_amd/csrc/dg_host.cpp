@@ -195,7 +195,8 @@ int dg_context_create(int device, dg_context_t** out) {
 	}
 
 	// CRC tables: slicing-by-8 and nibble tables of the combine constants
-	std::vector<uint64_t> tab(8 * 256 + kCrcLevels * kCrcNibTabWords);
+	// + the finaliser's constants: x^(8 kCrcSegBytes) and the 16 pad inverses
+	std::vector<uint64_t> tab(8 * 256 + (kCrcLevels + 1 + 16) * kCrcNibTabWords);
 	for (int i = 0; i < 256; ++i) {
 		uint64_t c = (uint64_t)i;
 		for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
@@ -220,6 +221,12 @@ int dg_context_create(int device, dg_context_t** out) {
 		xinv[t] = z;
 	}
 	ctx->kseg = gf2_xpow(8ull * kCrcSegBytes);
+	for (int c = 0; c < 17; ++c) {   // nibble tables: kseg, then xinv[0..15]
+		const uint64_t K = c == 0 ? ctx->kseg : xinv[c - 1];
+		for (int j = 0; j < 16; ++j)
+			for (int nb = 0; nb < 16; ++nb)
+				tab[8 * 256 + (kCrcLevels + c) * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
+	}
 	if (hipMalloc(&ctx->d_crc_tables, tab.size() * 8) != hipSuccess ||
 	    hipMalloc(&ctx->d_xinv, sizeof xinv) != hipSuccess ||
 	    hipMemcpy(ctx->d_crc_tables, tab.data(), tab.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||

@@ -279,16 +279,6 @@ __device__ __forceinline__ uint64_t mul_nib(uint64_t c, const uint64_t* __restri
 	return r;
 }
 
-// a * b mod P in the reflected representation (MSB = x^0), bit-serial.
-__device__ uint64_t gf2_mulmod(uint64_t a, uint64_t b) {
-	uint64_t p = 0;
-	for (int i = 0; i < 64; ++i) {
-		if ((a >> (63 - i)) & 1) p ^= b;
-		b = (b & 1) ? (b >> 1) ^ kCrcPoly : (b >> 1);
-	}
-	return p;
-}
-
 // keep-mask of bytes [lo, hi) within an 8-byte word (0 <= lo, hi <= 8)
 __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
 	lo = lo < 0 ? 0 : lo;   // clamp first: a negative shift count is undefined
@@ -400,12 +390,15 @@ __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
 		for (uint64_t k = 0; k < sp.len; ++k) c = a.tables[(uint8_t)(c ^ d[k])] ^ (c >> 8);
 		crc = ~c;
 	} else {
+		// constant multiplications by nibble tables (16 cached loads instead
+		// of a 64-step bit-serial product), skipped where they are trivial
+		const uint64_t* KS = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;   // x^(8 kCrcSegBytes)
 		uint64_t acc = 0;
 		for (uint32_t j = 0; j < sp.nseg; ++j)
-			acc = gf2_mulmod(a.kseg, acc) ^ a.seg_crc[sp.seg_base + j];
+			acc = (j ? mul_nib(acc, KS) : 0ull) ^ a.seg_crc[sp.seg_base + j];
 		const uintptr_t end = (uintptr_t)(a.arena[sp.which] + sp.off) + sp.len;
 		const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
-		acc = gf2_mulmod(a.xinv[t], acc);   // undo the trailing pad bytes
+		if (t) acc = mul_nib(acc, KS + (1 + t) * kCrcNibTabWords);   // undo the trailing pad bytes (x^-8t)
 		crc = ~acc;
 	}
 	a.out[i] = crc;
