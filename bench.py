@@ -393,7 +393,8 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    out.zero_()
+    out.zero_()                 # (torch's stream: finished before the decode's stream starts)
+    torch.cuda.synchronize()
     step()
     torch.cuda.synchronize()
     if int(status.abs().sum()) != 0 or not torch.equal(out, ver[:n * L]):
@@ -407,9 +408,10 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     dec_ms = stages.get("decode", 0.0)
     # decode_kernel algorithmic bytes: the deltas read, the initial R image
     # written, COPY sources read and the outputs written (in place: the
-    # output buffer starts as R) -> |delta| + |R| + 2 |V|
+    # output buffer starts as R), then R and the output read again by the
+    # in-kernel CRC-64/XZ checks -> |delta| + 2 |R| + 3 |V|
     r_bytes = sum(rl for _, rl, _, _ in layout)
-    alg = d_bytes + r_bytes + 2 * v_bytes
+    alg = d_bytes + 2 * r_bytes + 3 * v_bytes
     achieved = alg / (dec_ms / 1e3) / 1e9 if dec_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(name, "decode_kernel") if npg == CONFIGS[name][0] else (None, None)
     line = {
@@ -428,7 +430,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg,
-                     "algorithmic_bytes_per_stream": "|delta| + |R| + 2 |V|",
+                     "algorithmic_bytes_per_stream": "|delta| + 2 |R| + 3 |V| (parse + apply + src/dst CRC in one kernel)",
                      "avg_launch_ms": round(dec_ms, 4),
                      "stage_ms": {k: round(v, 4) for k, v in stages.items()}},
         "cpu_baseline": None,

@@ -63,6 +63,9 @@ struct CrcSpanDev {
 // tab[c][16*j + n] = (n << 4j) * K_c mod P  (reflected), see dg_host.cpp.
 constexpr int kCrcLevels = 6;          // in-wave tree levels
 constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
+// after the level tables: x^(8 kCrcSegBytes), x^(-8t) for t = 0..15, and
+// x^(8 kCrcSegBytes k) for k = 2..4 (the block-level span CRC of decode)
+constexpr int kCrcFinTabs = 1 + 16 + 3;
 
 
 struct EncodeArgs {
@@ -206,8 +209,9 @@ struct DecodeArgs {
 	uint8_t* out;
 	uint64_t* out_len;
 	int32_t* status;
-	CrcSpanDev* out_spans;     // nullable: span i's length := version size (for the dst CRC)
 	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
+	const uint64_t* tables;    // CRC tables (CrcArgs::tables); with crc_check
+	uint32_t crc_check;        // 1: src/dst CRC-64/XZ computed and checked in-kernel (main.c:341-385)
 };
 
 struct SynthSpan {   // synthetic R stream: splitmix64(seed) words at off
@@ -243,9 +247,6 @@ hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_
                             const int32_t* status, uint32_t n, hipStream_t st);
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
-hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
-                                const uint64_t* ref_crc, const uint64_t* out_crc, int32_t* status,
-                                hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);
 hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,

@@ -196,7 +196,7 @@ int dg_context_create(int device, dg_context_t** out) {
 
 	// CRC tables: slicing-by-8 and nibble tables of the combine constants
 	// + the finaliser's constants: x^(8 kCrcSegBytes) and the 16 pad inverses
-	std::vector<uint64_t> tab(8 * 256 + (kCrcLevels + 1 + 16) * kCrcNibTabWords);
+	std::vector<uint64_t> tab(8 * 256 + (kCrcLevels + kCrcFinTabs) * kCrcNibTabWords);
 	for (int i = 0; i < 256; ++i) {
 		uint64_t c = (uint64_t)i;
 		for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
@@ -221,8 +221,8 @@ int dg_context_create(int device, dg_context_t** out) {
 		xinv[t] = z;
 	}
 	ctx->kseg = gf2_xpow(8ull * kCrcSegBytes);
-	for (int c = 0; c < 17; ++c) {   // nibble tables: kseg, then xinv[0..15]
-		const uint64_t K = c == 0 ? ctx->kseg : xinv[c - 1];
+	for (int c = 0; c < kCrcFinTabs; ++c) {   // nibble tables: kseg, xinv[0..15], kseg^2..4
+		const uint64_t K = c == 0 ? ctx->kseg : c <= 16 ? xinv[c - 1] : gf2_xpow(8ull * kCrcSegBytes * (uint64_t)(c - 15));
 		for (int j = 0; j < 16; ++j)
 			for (int nb = 0; nb < 16; ++nb)
 				tab[8 * 256 + (kCrcLevels + c) * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
@@ -1009,12 +1009,8 @@ void dg_encode_plan_destroy(dg_encode_plan_t* P) {
 	if (!P) return;
 	hipSetDevice(P->ctx->device);
 	hipStreamSynchronize(P->ctx->stream);
-	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
-	if (P->ev_fork) hipEventDestroy(P->ev_fork);
-	if (P->ev_join) hipEventDestroy(P->ev_join);
-	if (P->side) hipStreamDestroy(P->side);
 	delete P;
 }
 
@@ -1065,13 +1061,7 @@ struct dg_decode_plan {
 	dg_context_t* ctx = nullptr;
 	uint32_t n = 0;
 	int ignore_hash = 0;
-	DevBuf d_desc;
-	// reference CRC (side stream) and output CRC (after decode)
-	DevBuf d_rspans, d_rsegs, d_rsegc, d_rcrc;
-	DevBuf d_ospans, d_osegs, d_osegc, d_ocrc;
-	uint32_t n_rsegs = 0, n_osegs = 0;
-	hipStream_t side = nullptr;
-	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	DevBuf d_desc;   // the decode kernel computes and checks both CRCs itself
 	bool timing = false;
 	std::vector<hipEvent_t> ev;
 	uint32_t slots = 0, runs = 0;
@@ -1099,50 +1089,15 @@ int dg_decode_plan_create(dg_context_t* ctx, const dg_decode_desc_t* descs, uint
 			delete P;
 			return set_err(ctx, DG_ERR_TOO_LARGE, "stream %u exceeds the u32 format", i);
 		}
-	std::vector<dg_span_t> rs(n), os(n);
-	std::vector<uint32_t> w0(n, 0), w1(n, 1);
-	for (uint32_t i = 0; i < n; ++i) {
-		rs[i] = dg_span_t{descs[i].ref_off, descs[i].ref_len};
-		os[i] = dg_span_t{descs[i].out_off, descs[i].out_cap};   // length patched on device
-	}
-	std::vector<CrcSpanDev> rsd, osd;
-	std::vector<CrcSegDev> rseg, oseg;
-	plan_crc_spans(rs, w0, rsd, rseg);
-	plan_crc_spans(os, w1, osd, oseg);
-	P->n_rsegs = (uint32_t)rseg.size();
-	P->n_osegs = (uint32_t)oseg.size();
 	const size_t nn = std::max<size_t>(n, 1);
-	int bad = 0;
-	bad |= P->d_desc.alloc(sizeof(dg_decode_desc_t) * nn);
-	bad |= P->d_rspans.alloc(sizeof(CrcSpanDev) * nn);
-	bad |= P->d_rsegs.alloc(sizeof(CrcSegDev) * std::max<size_t>(rseg.size(), 1));
-	bad |= P->d_rsegc.alloc(8 * std::max<size_t>(rseg.size(), 1));
-	bad |= P->d_rcrc.alloc(8 * nn);
-	bad |= P->d_ospans.alloc(sizeof(CrcSpanDev) * nn);
-	bad |= P->d_osegs.alloc(sizeof(CrcSegDev) * std::max<size_t>(oseg.size(), 1));
-	bad |= P->d_osegc.alloc(8 * std::max<size_t>(oseg.size(), 1));
-	bad |= P->d_ocrc.alloc(8 * nn);
-	if (bad) {
+	if (P->d_desc.alloc(sizeof(dg_decode_desc_t) * nn)) {
 		delete P;
 		return set_err(ctx, DG_ERR_NOMEM, "device allocation failed");
 	}
 	hipStream_t st = ctx->stream;
 	hipError_t e = hipSuccess;
-	if (n) {
-		e = hipMemcpyAsync(P->d_desc.p, descs, sizeof(dg_decode_desc_t) * n, hipMemcpyHostToDevice, st);
-		if (e == hipSuccess) e = hipMemcpyAsync(P->d_rspans.p, rsd.data(), sizeof(CrcSpanDev) * n, hipMemcpyHostToDevice, st);
-		// output spans: segmentation sized for out_cap; every run's decoder
-		// rewrites each span's length from its delta header before the CRC
-		if (e == hipSuccess) e = hipMemcpyAsync(P->d_ospans.p, osd.data(), sizeof(CrcSpanDev) * n, hipMemcpyHostToDevice, st);
-		if (e == hipSuccess && !rseg.empty())
-			e = hipMemcpyAsync(P->d_rsegs.p, rseg.data(), sizeof(CrcSegDev) * rseg.size(), hipMemcpyHostToDevice, st);
-		if (e == hipSuccess && !oseg.empty())
-			e = hipMemcpyAsync(P->d_osegs.p, oseg.data(), sizeof(CrcSegDev) * oseg.size(), hipMemcpyHostToDevice, st);
-	}
+	if (n) e = hipMemcpyAsync(P->d_desc.p, descs, sizeof(dg_decode_desc_t) * n, hipMemcpyHostToDevice, st);
 	if (e == hipSuccess) e = hipStreamSynchronize(st);
-	if (e == hipSuccess) e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
-	if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
-	if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_join, hipEventDisableTiming);
 	if (e != hipSuccess) {
 		dg_decode_plan_destroy(P);
 		return set_err(ctx, DG_ERR_HIP, "decode plan setup failed: %s", hipGetErrorString(e));
@@ -1205,36 +1160,16 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
 	hipEvent_t* ev = nullptr;
 	if (P->timing) ev = &P->ev[(size_t)kDecEvents * (P->runs++ % P->slots)];
-	auto crc_args = [&](const uint8_t* arena, DevBuf& spans, DevBuf& segs, uint32_t nsegs, DevBuf& segc,
-	                    DevBuf& outc) {
-		CrcArgs a{};
-		a.arena[0] = a.arena[1] = arena;
-		a.spans = spans.as<CrcSpanDev>();
-		a.segs = segs.as<CrcSegDev>();
-		a.n_segs = nsegs;
-		a.n_spans = P->n;
-		a.tables = ctx->d_crc_tables;
-		a.seg_crc = segc.as<uint64_t>();
-		a.out = outc.as<uint64_t>();
-		a.xinv = ctx->d_xinv;
-		a.kseg = ctx->kseg;
-		return a;
-	};
 	const bool check = !P->ignore_hash;
-	if (check) {   // 1. CRC of every reference span, forked (main.c:341-356)
-		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
-		HIPCHK(ctx, hipStreamWaitEvent(P->side, P->ev_fork, 0));
-		if (ev) HIPCHK(ctx, hipEventRecord(ev[0], P->side));
-		HIPCHK(ctx, launch_crc(crc_args(d_ref, P->d_rspans, P->d_rsegs, P->n_rsegs, P->d_rsegc, P->d_rcrc),
-		                       P->side));
-		if (ev) HIPCHK(ctx, hipEventRecord(ev[1], P->side));
-		HIPCHK(ctx, hipEventRecord(P->ev_join, P->side));
-	} else if (ev) {
+	// parse + apply (encoding.c:111-178, apply.c:229-284), then the CRC-64/XZ
+	// of R and of the output, checked against the header in the same kernel
+	// (main.c:341-356, :376-385); --ignore-hash skips the CRCs.  The ref_crc
+	// and out_crc+verify stages are empty (kept for the timing layout).
+	if (ev) {
 		HIPCHK(ctx, hipEventRecord(ev[0], st));
 		HIPCHK(ctx, hipEventRecord(ev[1], st));
+		HIPCHK(ctx, hipEventRecord(ev[2], st));
 	}
-	// 2. parse + apply (encoding.c:111-178, apply.c:229-284)
-	if (ev) HIPCHK(ctx, hipEventRecord(ev[2], st));
 	DecodeArgs a{};
 	{
 		static const uint32_t dbg = [] {
@@ -1250,16 +1185,10 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	a.out = d_out;
 	a.out_len = d_out_len;
 	a.status = d_status;
-	a.out_spans = check ? P->d_ospans.as<CrcSpanDev>() : nullptr;
+	a.tables = ctx->d_crc_tables;
+	a.crc_check = check ? 1u : 0u;
 	HIPCHK(ctx, launch_decode(a, st));
 	if (ev) HIPCHK(ctx, hipEventRecord(ev[3], st));
-	// 3. CRC of every output, then the checks (main.c:376-385)
-	if (check) {
-		HIPCHK(ctx, launch_crc(crc_args(d_out, P->d_ospans, P->d_osegs, P->n_osegs, P->d_osegc, P->d_ocrc), st));
-		HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
-		HIPCHK(ctx, launch_decode_verify(d_delta, a.descs, P->n, P->d_rcrc.as<uint64_t>(),
-		                                 P->d_ocrc.as<uint64_t>(), d_status, st));
-	}
 	if (ev) HIPCHK(ctx, hipEventRecord(ev[4], st));
 	return DG_OK;
 }
@@ -1268,12 +1197,8 @@ void dg_decode_plan_destroy(dg_decode_plan_t* P) {
 	if (!P) return;
 	hipSetDevice(P->ctx->device);
 	hipStreamSynchronize(P->ctx->stream);
-	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
-	if (P->ev_fork) hipEventDestroy(P->ev_fork);
-	if (P->ev_join) hipEventDestroy(P->ev_join);
-	if (P->side) hipStreamDestroy(P->side);
 	delete P;
 }
 

@@ -296,26 +296,18 @@ __device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint6
 	       T[(x >> 24) & 0xff] ^ (x >> 32);
 }
 
-// Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
-// and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
-// tables read through the cache, at most 64 VGPRs.
-__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
-	__shared__ uint64_t T[4 * 256];
-	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6;
+// The raw CRC (init 0) of segment j of nseg of the span [start, start + len)
+// (len >= 8; the span's first 8 bytes inverted: init = ~0) by one wave: each
+// lane folds kCrcLaneBytes of it, then an in-wave tree.  Uniform result.
+// T: the slicing-by-4 tables (LDS), L: the level nibble tables.
+__device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
+                                                 const uint64_t* T, const uint64_t* L) {
 	const uint32_t lane = lane_id();
-	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
-	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
-	     seg += gridDim.x * kCrcWavesPerBlock) {
-	const CrcSegDev sd = a.segs[seg];
-	const CrcSpanDev sp = a.spans[sd.span];
-	const uintptr_t start = (uintptr_t)(a.arena[sp.which] + sp.off);
-	const uintptr_t end = start + sp.len;
+	const uintptr_t end = start + len;
 	const uintptr_t a0 = start & ~(uintptr_t)15;
 	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)sp.nseg * kCrcSegBytes;   // may wrap below a0
-	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
+	const uintptr_t dom = a1 - (uintptr_t)nseg * kCrcSegBytes;   // may wrap below a0
+	const uintptr_t cs = dom + (uintptr_t)j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
 
 	uint64_t reg = 0;
 	constexpr int kPf = 4;   // 16-byte loads in flight per lane
@@ -365,7 +357,6 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 		}
 	}
 	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
-	const uint64_t* L = a.tables + 8 * 256;
 #pragma unroll
 	for (int lv = 0; lv < kCrcLevels; ++lv) {
 		const int d = 1 << lv;
@@ -375,7 +366,31 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 		const uint64_t shifted = mul_nib(reg, L + lv * kCrcNibTabWords);
 		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
 	}
-	if (lane == 0) a.seg_crc[seg] = reg;
+	return uni64(reg);
+}
+
+// segments of a span of len >= 8 bytes at start
+__device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len) {
+	const uintptr_t a0 = start & ~(uintptr_t)15, a1 = (start + len + 15) & ~(uintptr_t)15;
+	return (uint32_t)((a1 - a0 + kCrcSegBytes - 1) / kCrcSegBytes);
+}
+
+// Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
+// and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
+// tables read through the cache, at most 64 VGPRs.
+__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
+	__shared__ uint64_t T[4 * 256];
+	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6;
+	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
+	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
+	     seg += gridDim.x * kCrcWavesPerBlock) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_wave((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, T,
+		                                a.tables + 8 * 256);
+		if (lane_id() == 0) a.seg_crc[seg] = c;
 	}
 }
 
@@ -699,6 +714,18 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 // The block barrier between windows also orders every store of one window
 // before the next window's reads and writes.
 constexpr uint32_t kDecBlock = 256;
+
+// A block barrier that also orders global memory between the block's waves:
+// every wave's stores are acknowledged (vmcnt counts stores on gfx9) before
+// any wave passes, and the CU's L1 is invalidated after, so loads of bytes
+// another wave of the block just wrote see them.  A plain __syncthreads
+// orders LDS only (its workgroup-scope fence waits for no global store), and
+// agent-scope fences would write back the XCD's L2 (~6x slower decode).
+__device__ __forceinline__ void block_sync_global() {
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	asm volatile("buffer_inv sc0" ::: "memory");
+}
 constexpr uint32_t kDecWaves = kDecBlock / 64;
 
 struct DecCmd {
@@ -882,6 +909,8 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	__shared__ uint16_t jumps[kDecMaxCmds / 8 + 1];
 	__shared__ uint32_t sh[8];   // walk results and window flags
 	__shared__ uint32_t bsum[2 * (kDecMaxCmds / 64 + 1)];   // per batch: first written dst, max end
+	__shared__ uint64_t cpart[2][kDecWaves];   // crc_check: per span, each wave's Horner partial
+	__shared__ uint32_t clast[2][kDecWaves];   // and its last segment
 	uint16_t* N2 = NX;
 	uint16_t* N4 = NX + kDecWin;
 	uint16_t* N8 = NX + 2 * kDecWin;
@@ -922,8 +951,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		if (tid == 0) {
 			a.status[i] = st;
 			a.out_len[i] = 0;
-			if (a.out_spans) a.out_spans[i].len = 0;
-		}
+			}
 		return;
 	}
 	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
@@ -954,7 +982,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		}
 		for (uint64_t k = k0 + tid; k < bsz; k += kDecBlock) O[k] = k < init ? R[k] : 0;
 	}
-	__syncthreads();   // every wave's image stores complete before any command store
+	block_sync_global();   // every wave's image stores complete before any command load or store
 	DPROF_ADD(DP_FILL, tf0);
 
 	uint64_t pos = 25;   // stream offset of the current window: a command boundary
@@ -1180,15 +1208,78 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			}
 		}
 		DPROF_T(tq2);
-		__syncthreads();   // the window's stores complete before the next window
+		block_sync_global();   // the window's stores complete before the next window
 		DPROF_ADD(DP_C_BAR, tq2);
 		DPROF_ADD(DP_COPY, tc0);
 		pos = next_pos;
 	}
+	// ── 7. CRC-64/XZ of R and of the output, checked against the header
+	//    (main.c:341-356 before the apply, :376-385 after; a source mismatch
+	//    takes precedence, the output is then unspecified).  Segment j of a
+	//    span goes to wave j % 4, which folds its segments Horner-wise by
+	//    x^(8 * 4 segments); thread 0 shifts the partials into place. ──
+	int32_t cst = 0;
+	if (a.crc_check && !st) {
+		block_sync_global();   // every wave's output stores before any CRC read
+		uint64_t* TS = reinterpret_cast<uint64_t*>(NX);   // slicing-by-4 tables in the dead doubling arrays
+		for (uint32_t k = tid; k < 4 * 256; k += kDecBlock) TS[k] = a.tables[k];
+		__syncthreads();
+		const uint64_t* Lv = a.tables + 8 * 256;
+		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
+		const uintptr_t sa[2] = {(uintptr_t)R, (uintptr_t)O};
+		const uint64_t sl[2] = {rl, vsize};
+#pragma unroll
+		for (int sp = 0; sp < 2; ++sp) {
+			uint64_t acc = 0;
+			uint32_t last = ~0u;
+			if (sl[sp] >= 8) {
+				const uint32_t nseg = crc_nseg(sa[sp], sl[sp]);
+				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
+					const uint64_t c = crc_seg_wave(sa[sp], sl[sp], nseg, j, TS, Lv);
+					acc = (last != ~0u ? mul_nib(acc, KF + 19 * kCrcNibTabWords) : 0ull) ^ c;
+					last = j;
+				}
+			}
+			if (lane == 0) {
+				cpart[sp][wave] = acc;
+				clast[sp][wave] = last;
+			}
+		}
+		__syncthreads();
+		if (tid == 0) {
+			uint64_t crc[2];
+			for (int sp = 0; sp < 2; ++sp) {
+				if (sl[sp] < 8) {
+					const uint8_t* d = reinterpret_cast<const uint8_t*>(sa[sp]);
+					uint64_t c = ~0ULL;
+					for (uint64_t k = 0; k < sl[sp]; ++k) c = a.tables[(uint8_t)(c ^ d[k])] ^ (c >> 8);
+					crc[sp] = ~c;
+					continue;
+				}
+				const uint32_t nseg = crc_nseg(sa[sp], sl[sp]);
+				uint64_t raw = 0;
+				for (uint32_t w2 = 0; w2 < kDecWaves; ++w2) {
+					if (clast[sp][w2] == ~0u) continue;
+					const uint32_t k = nseg - 1 - clast[sp][w2];   // 0..3 segments after its last
+					raw ^= k == 0 ? cpart[sp][w2]
+					              : mul_nib(cpart[sp][w2], KF + (k == 1 ? 0 : 15 + k) * kCrcNibTabWords);
+				}
+				const uintptr_t end = sa[sp] + sl[sp];
+				const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
+				if (t) raw = mul_nib(raw, KF + (1 + t) * kCrcNibTabWords);   // undo the trailing pad
+				crc[sp] = ~raw;
+			}
+			uint64_t sc = 0, dc = 0;
+			for (int k = 0; k < 8; ++k) {
+				sc = (sc << 8) | D[9 + k];
+				dc = (dc << 8) | D[17 + k];
+			}
+			cst = sc != crc[0] ? 9 : (dc != crc[1] ? 10 : 0);
+		}
+	}
 	if (tid == 0) {
-		a.status[i] = st;
+		a.status[i] = st ? st : cst;
 		a.out_len[i] = st ? 0 : vsize;
-		if (a.out_spans) a.out_spans[i].len = st ? 0 : vsize;
 	}
 #ifdef DG_ONEPASS_PROF
 	{
@@ -1202,41 +1293,12 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 #endif
 }
 
-// CRC checks after decoding, in the reference's order of precedence: a
-// malformed stream (set by the decoder) first, then the source pre-check
-// (main.c:341-356), then the output post-check (main.c:379-385).  Either CRC
-// array may be null (--ignore-hash).  On a source mismatch the reference stops
-// before applying; here the output buffer content is unspecified.
-__global__ __launch_bounds__(64) void decode_verify_kernel(const uint8_t* delta,
-                                                           const dg_decode_desc_dev* descs,
-                                                           uint32_t n, const uint64_t* ref_crc,
-                                                           const uint64_t* out_crc,
-                                                           int32_t* status) {
-	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-	if (i >= n || status[i] != 0) return;
-	const uint8_t* D = delta + descs[i].delta_off;
-	uint64_t sc = 0, dc = 0;
-	for (int k = 0; k < 8; ++k) {
-		sc = (sc << 8) | D[9 + k];
-		dc = (dc << 8) | D[17 + k];
-	}
-	if (ref_crc && sc != ref_crc[i]) status[i] = 9;
-	else if (out_crc && dc != out_crc[i]) status[i] = 10;
-}
-
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st) {
 	if (a.n) hipLaunchKernelGGL(decode_kernel, dim3(a.n), dim3(kDecBlock), 0, st, a);
 	return hipGetLastError();
 }
 
-hipError_t launch_decode_verify(const uint8_t* delta, const dg_decode_desc_dev* descs, uint32_t n,
-                                const uint64_t* ref_crc, const uint64_t* out_crc, int32_t* status,
-                                hipStream_t st) {
-	if (n)
-		hipLaunchKernelGGL(decode_verify_kernel, dim3((n + 63) / 64), dim3(64), 0, st, delta, descs, n,
-		                   ref_crc, out_crc, status);
-	return hipGetLastError();
-}
+
 
 
 }  // namespace dg
