@@ -486,8 +486,11 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 		bool myok = false;   // this lane's member verified
 		if (mine) {
 			mem_s[lane] = (uint32_t)(g0 + (int64_t)s);
-			if (!known || T >= 64u * kLongChunks)   // unverified: the chain runs its epoch exactly
-				*(uint4*)(srec + 4 * lane) = make_uint4(0u, 0u, 0u, 0u);
+			if (!known || T >= 64u * kLongChunks) {   // unverified: the chain runs its epoch exactly
+				uint32_t z;   // a zero made here: a hoisted constant uint4 was spilled to scratch
+				asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+				*(uint4*)(srec + 4 * lane) = make_uint4(z, z, z, z);
+			}
 		}
 
 		// ── short members, packed 64 steps per round (lane = step) ──

@@ -14,19 +14,21 @@ import os
 import sys
 
 out_dir, tag, cfg, kre = sys.argv[1:5]
+label = sys.argv[5] if len(sys.argv) > 5 else kre   # the "kernel" field bench.py matches
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    xs = []
+    per = {}   # kernel name -> values per dispatch; a regex matching several
     for f in glob.glob(os.path.join(out_dir, c, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             if row["Counter_Name"] == c:
-                xs.append(float(row["Counter_Value"]))
-    vals[c] = sum(xs) / len(xs) if xs else None
-    vals[c + "_dispatches"] = len(xs)
+                per.setdefault(row.get("Kernel_Name", ""), []).append(float(row["Counter_Value"]))
+    # kernels (one launch of each per step) sums their per-dispatch means
+    vals[c] = sum(sum(x) / len(x) for x in per.values()) if per else None
+    vals[c + "_dispatches"] = sum(len(x) for x in per.values())
 fetch = vals["FETCH_SIZE"] * 1024 * 2 if vals["FETCH_SIZE"] is not None else None
 write = vals["WRITE_SIZE"] * 1024 if vals["WRITE_SIZE"] is not None else None
 res = {
-    "kernel": kre, "config": cfg,
+    "kernel": label, "config": cfg, "kernel_regex": kre,
     "fetch_size_kib_raw": vals["FETCH_SIZE"], "write_size_kib_raw": vals["WRITE_SIZE"],
     "dispatches": [vals["FETCH_SIZE_dispatches"], vals["WRITE_SIZE_dispatches"]],
     "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,

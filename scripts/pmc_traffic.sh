@@ -4,7 +4,7 @@
 # passes, no trace domains mixed in).  Summarised by scripts/pmc_traffic.py
 # into profiles/<tag>_pmc_traffic_<config>.json, which bench.py reports as
 # roofline.traffic.
-# usage: scripts/pmc_traffic.sh TAG CONFIG KERNEL_REGEX
+# usage: scripts/pmc_traffic.sh TAG CONFIG KERNEL_REGEX [LABEL]
 set -o pipefail
 TAG=${1:-r01}
 CFG=${2:-c2}
@@ -17,4 +17,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
       -d $OUT/$c -o pmc -- python3 bench.py --config $CFG --also none --steps 5 --warmup 1 --no-cpu-baseline \
       > $OUT/$c.log 2>&1 || { echo "pass $c failed rc=$?"; tail -5 $OUT/$c.log; exit 1; }
 done
-python3 scripts/pmc_traffic.py $OUT $TAG $CFG "$KRE"
+python3 scripts/pmc_traffic.py $OUT $TAG $CFG "$KRE" "${4:-$KRE}"
