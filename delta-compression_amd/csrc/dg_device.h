@@ -63,9 +63,11 @@ struct CrcSpanDev {
 // tab[c][16*j + n] = (n << 4j) * K_c mod P  (reflected), see dg_host.cpp.
 constexpr int kCrcLevels = 6;          // in-wave tree levels
 constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
-// after the level tables: x^(8 kCrcSegBytes), x^(-8t) for t = 0..15, and
-// x^(8 kCrcSegBytes k) for k = 2..4 (the block-level span CRC of decode)
-constexpr int kCrcFinTabs = 1 + 16 + 3;
+// after the level tables (F): x^(8 kCrcSegBytes), x^(-8t) for t = 0..15,
+// x^(8 kCrcSegBytes k) for k = 2..4, then for the decode kernel's 256-byte
+// lanes x^(8 * 256), x^(8 * 512) (its first two tree levels) and x^(8 * 48 KiB)
+constexpr int kCrcFinTabs = 1 + 16 + 3 + 3;
+constexpr int kCrcFinX256 = 20, kCrcFinX512 = 21, kCrcFinX48K = 22;   // indices in F
 
 
 struct EncodeArgs {

@@ -221,8 +221,12 @@ int dg_context_create(int device, dg_context_t** out) {
 		xinv[t] = z;
 	}
 	ctx->kseg = gf2_xpow(8ull * kCrcSegBytes);
-	for (int c = 0; c < kCrcFinTabs; ++c) {   // nibble tables: kseg, xinv[0..15], kseg^2..4
-		const uint64_t K = c == 0 ? ctx->kseg : c <= 16 ? xinv[c - 1] : gf2_xpow(8ull * kCrcSegBytes * (uint64_t)(c - 15));
+	for (int c = 0; c < kCrcFinTabs; ++c) {   // nibble tables: kseg, xinv[0..15], kseg^2..4, x^(8*256|512|48Ki)
+		const uint64_t K = c == 0 ? ctx->kseg
+		                 : c <= 16 ? xinv[c - 1]
+		                 : c <= 19 ? gf2_xpow(8ull * kCrcSegBytes * (uint64_t)(c - 15))
+		                 : c == kCrcFinX256 ? gf2_xpow(8ull * 256)
+		                 : c == kCrcFinX512 ? gf2_xpow(8ull * 512) : gf2_xpow(8ull * 48 * 1024);
 		for (int j = 0; j < 16; ++j)
 			for (int nb = 0; nb < 16; ++nb)
 				tab[8 * 256 + (kCrcLevels + c) * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));

@@ -296,18 +296,23 @@ __device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint6
 	       T[(x >> 24) & 0xff] ^ (x >> 32);
 }
 
-// The raw CRC (init 0) of segment j of nseg of the span [start, start + len)
-// (len >= 8; the span's first 8 bytes inverted: init = ~0) by one wave: each
-// lane folds kCrcLaneBytes of it, then an in-wave tree.  Uniform result.
-// T: the slicing-by-4 tables (LDS), L: the level nibble tables.
+// The raw CRC (init 0) of segment j of nseg (64 LB bytes each) of the span
+// [start, start + len) (len >= 8; the span's first 8 bytes inverted: init =
+// ~0) by one wave: each lane folds LB bytes, then an in-wave tree.  Uniform
+// result.  T: the slicing-by-4 tables (LDS); tree: the tree's nibble tables,
+// level l = x^(8 LB 2^l) at tree + 256 l (the context's level tables for
+// 1 KiB lanes; an LDS copy in the decode kernel).
+template <uint32_t LB = kCrcLaneBytes>
 __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                 const uint64_t* T, const uint64_t* L) {
+                                                 const uint64_t* T, const uint64_t* tree) {
+	constexpr uint32_t kLaneBytes = LB;
+	constexpr uint64_t kSeg = 64ull * LB;
 	const uint32_t lane = lane_id();
 	const uintptr_t end = start + len;
 	const uintptr_t a0 = start & ~(uintptr_t)15;
 	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)nseg * kCrcSegBytes;   // may wrap below a0
-	const uintptr_t cs = dom + (uintptr_t)j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
+	const uintptr_t dom = a1 - (uintptr_t)nseg * kSeg;   // may wrap below a0
+	const uintptr_t cs = dom + (uintptr_t)j * kSeg + (uintptr_t)lane * kLaneBytes;
 
 	uint64_t reg = 0;
 	constexpr int kPf = 4;   // 16-byte loads in flight per lane
@@ -317,12 +322,12 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 	typedef __attribute__((address_space(1))) const uint64_t gcu64;   // global, not flat: loads
 	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
 	auto clamp32 = [](intptr_t v) -> int32_t {
-		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kCrcLaneBytes + 64 ? (intptr_t)kCrcLaneBytes + 64 : v));
+		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kLaneBytes + 64 ? (intptr_t)kLaneBytes + 64 : v));
 	};
 	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
 	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
 	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
-	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
+	for (uint32_t w0 = 0; w0 < kLaneBytes; w0 += 16 * kPf) {
 		ulonglong2 xs[kPf];
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
@@ -363,16 +368,16 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 		const uint32_t plo = (uint32_t)__shfl_down((int)(uint32_t)reg, d, 64);
 		const uint32_t phi = (uint32_t)__shfl_down((int)(uint32_t)(reg >> 32), d, 64);
 		const uint64_t right = ((uint64_t)phi << 32) | plo;
-		const uint64_t shifted = mul_nib(reg, L + lv * kCrcNibTabWords);
+		const uint64_t shifted = mul_nib(reg, tree + lv * kCrcNibTabWords);
 		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
 	}
 	return uni64(reg);
 }
 
-// segments of a span of len >= 8 bytes at start
-__device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len) {
+// segments of seg bytes of a span of len >= 8 bytes at start
+__device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len, uint64_t seg) {
 	const uintptr_t a0 = start & ~(uintptr_t)15, a1 = (start + len + 15) & ~(uintptr_t)15;
-	return (uint32_t)((a1 - a0 + kCrcSegBytes - 1) / kCrcSegBytes);
+	return (uint32_t)((a1 - a0 + seg - 1) / seg);
 }
 
 // Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
@@ -714,6 +719,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 // The block barrier between windows also orders every store of one window
 // before the next window's reads and writes.
 constexpr uint32_t kDecBlock = 256;
+constexpr uint32_t kDecCrcLane = 256;                 // in-kernel CRC: bytes per lane
+constexpr uint64_t kDecCrcSeg = 64ull * kDecCrcLane;  // 16 KiB segments
+static_assert(4 * kDecCrcSeg == kCrcSegBytes, "the Horner step (4 segments) is x^(8 kCrcSegBytes)");
 
 // A block barrier that also orders global memory between the block's waves:
 // every wave's stores are acknowledged (vmcnt counts stores on gfx9) before
@@ -1215,17 +1223,32 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	}
 	// ── 7. CRC-64/XZ of R and of the output, checked against the header
 	//    (main.c:341-356 before the apply, :376-385 after; a source mismatch
-	//    takes precedence, the output is then unspecified).  Segment j of a
-	//    span goes to wave j % 4, which folds its segments Horner-wise by
-	//    x^(8 * 4 segments); thread 0 shifts the partials into place. ──
+	//    takes precedence, the output is then unspecified).  Segments of
+	//    16 KiB (256-byte lanes: a quarter of the encode CRC's serial chain
+	//    per lane, every wave busy on a 64 KiB stream); segment j of a span
+	//    goes to wave j % 4, which folds its segments Horner-wise by
+	//    x^(8 * 64 KiB); thread 0 shifts the partials into place. ──
 	int32_t cst = 0;
 	if (a.crc_check && !st) {
 		block_sync_global();   // every wave's output stores before any CRC read
-		uint64_t* TS = reinterpret_cast<uint64_t*>(NX);   // slicing-by-4 tables in the dead doubling arrays
-		for (uint32_t k = tid; k < 4 * 256; k += kDecBlock) TS[k] = a.tables[k];
-		__syncthreads();
 		const uint64_t* Lv = a.tables + 8 * 256;
 		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
+		// LDS (the dead doubling arrays, 22 of 24 KiB): the slicing-by-4
+		// tables, the tree's levels x^(8 * 256 * 2^l) and x^(8 * 64 KiB)
+		uint64_t* TS = reinterpret_cast<uint64_t*>(NX);
+		uint64_t* TT = TS + 4 * 256;
+		uint64_t* TK = TT + kCrcLevels * kCrcNibTabWords;
+		static_assert(8 * (4 * 256 + (kCrcLevels + 1) * kCrcNibTabWords) <= sizeof(NX), "CRC tables fit NX");
+		for (uint32_t k = tid; k < 4 * 256; k += kDecBlock) TS[k] = a.tables[k];
+		for (uint32_t k = tid; k < (kCrcLevels + 1) * kCrcNibTabWords; k += kDecBlock) {
+			const uint32_t lv = k / kCrcNibTabWords, e = k % kCrcNibTabWords;
+			const uint64_t* src = lv == 0 ? KF + kCrcFinX256 * kCrcNibTabWords
+			                    : lv == 1 ? KF + kCrcFinX512 * kCrcNibTabWords
+			                    : lv < kCrcLevels ? Lv + (lv - 2) * kCrcNibTabWords
+			                                      : KF;   // x^(8 * 64 KiB)
+			TT[k] = src[e];
+		}
+		__syncthreads();
 		const uintptr_t sa[2] = {(uintptr_t)R, (uintptr_t)O};
 		const uint64_t sl[2] = {rl, vsize};
 #pragma unroll
@@ -1233,10 +1256,10 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			uint64_t acc = 0;
 			uint32_t last = ~0u;
 			if (sl[sp] >= 8) {
-				const uint32_t nseg = crc_nseg(sa[sp], sl[sp]);
+				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
-					const uint64_t c = crc_seg_wave(sa[sp], sl[sp], nseg, j, TS, Lv);
-					acc = (last != ~0u ? mul_nib(acc, KF + 19 * kCrcNibTabWords) : 0ull) ^ c;
+					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, TS, TT);
+					acc = (last != ~0u ? mul_nib(acc, TK) : 0ull) ^ c;   // TK: x^(8 * 64 KiB) = 4 segments
 					last = j;
 				}
 			}
@@ -1256,13 +1279,15 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 					crc[sp] = ~c;
 					continue;
 				}
-				const uint32_t nseg = crc_nseg(sa[sp], sl[sp]);
+				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				uint64_t raw = 0;
 				for (uint32_t w2 = 0; w2 < kDecWaves; ++w2) {
 					if (clast[sp][w2] == ~0u) continue;
-					const uint32_t k = nseg - 1 - clast[sp][w2];   // 0..3 segments after its last
+					const uint32_t k = nseg - 1 - clast[sp][w2];   // 0..3 segments (16, 32, 48 KiB) after its last
 					raw ^= k == 0 ? cpart[sp][w2]
-					              : mul_nib(cpart[sp][w2], KF + (k == 1 ? 0 : 15 + k) * kCrcNibTabWords);
+					              : mul_nib(cpart[sp][w2], k == 1 ? Lv + 4 * kCrcNibTabWords      // x^(8 * 16 KiB)
+					                                       : k == 2 ? Lv + 5 * kCrcNibTabWords    // x^(8 * 32 KiB)
+					                                                : KF + kCrcFinX48K * kCrcNibTabWords);
 				}
 				const uintptr_t end = sa[sp] + sl[sp];
 				const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
