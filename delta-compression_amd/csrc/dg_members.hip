@@ -88,14 +88,30 @@ __device__ __forceinline__ void lds_fence() {
 // is V(c) == V(T) and V(T) == R(l) is R(T) == R(l), both plain ballots at T;
 // the other pairs (c, l != T) can exist only for an R hash in the filter, and
 // those rare flagged steps are resolved exactly with ballots.
+// Probes: the hash's low bits, and a 24x24 multiplicative mix of its bits
+// 8..31 (v_mul_u32_u24, full rate, instead of the quarter-rate v_mul_lo_u32):
+// between them every hash bit reaches a probe, so the V and R windows of one
+// step, whose hashes differ in the few bits a mismatched byte flips, do not
+// share both probes.
 template <uint32_t W>
 struct VFilter {
+	static constexpr uint32_t kLg = W == 64 ? 11u : (W == 128 ? 12u : 13u);
 	uint32_t* f;   // W words
 	__device__ void clear() {
 		for (uint32_t i = lane_id(); i < W; i += 64) f[i] = 0u;
 	}
-	__device__ void add(uint32_t h) { bloom_add<W>(f, h); }
-	__device__ bool has(uint32_t h) const { return bloom_has<W>(f, h); }
+	__device__ static uint32_t h2(uint32_t h) {
+		return __umul24(__builtin_amdgcn_alignbit(h, h, 8), 0x9E3779u) >> (32u - kLg);
+	}
+	__device__ void add(uint32_t h) {
+		const uint32_t a = h & (32u * W - 1u), b = h2(h);
+		atomicOr(&f[a >> 5], 1u << (a & 31u));
+		atomicOr(&f[b >> 5], 1u << (b & 31u));
+	}
+	__device__ bool has(uint32_t h) const {
+		const uint32_t a = h & (32u * W - 1u), b = h2(h);
+		return ((f[a >> 5] >> (a & 31u)) & (f[b >> 5] >> (b & 31u)) & 1u) != 0u;
+	}
 };
 
 // Intra-wave LDS hand-offs (lane A stores, lane B loads) need only program
