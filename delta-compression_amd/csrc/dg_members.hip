@@ -101,7 +101,8 @@ struct VFilter {
 		for (uint32_t i = lane_id(); i < W; i += 64) f[i] = 0u;
 	}
 	__device__ static uint32_t h2(uint32_t h) {
-		return __umul24(__builtin_amdgcn_alignbit(h, h, 8), 0x9E3779u) >> (32u - kLg);
+		// (HIP's __umul24 returns int: shift the product as unsigned)
+		return (uint32_t)__umul24(__builtin_amdgcn_alignbit(h, h, 8), 0x9E3779u) >> (32u - kLg);
 	}
 	__device__ void add(uint32_t h) {
 		const uint32_t a = h & (32u * W - 1u), b = h2(h);
