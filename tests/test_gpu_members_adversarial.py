@@ -1,0 +1,62 @@
+"""Member-mode onepass on data built to break the member checks.
+
+The verified-members path (dg_members.hip) accepts a member only when
+(A) no V window of a step equals an R window of another step of the member
+and (B) the T step is the first writer of its slot in one of the tables
+(onepass.c:141-219).  On random data both always hold, so the full-size C2/C3
+batches cannot tell a weakened check from a correct one.  These pairs make
+(A) and (B) fail often: periodic data (windows repeat at the period, inside
+one member), low-entropy alphabets, and tiny table sizes (slot collisions).
+Every delta is compared with the oracle; the chain mode runs the same pairs.
+"""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ONEPASS = 1
+
+
+def _periodic(rng, n, period):
+    unit = rng.randbytes(period)
+    return (unit * (n // period + 1))[:n]
+
+
+def _edit(rng, R, rate):
+    """Substitutions by bytes drawn from R itself, so an edited V window can
+    equal an R window elsewhere (a window holding a mismatch can only verify
+    a lookup if it is byte-equal to one, onepass.c:186,212)."""
+    V = bytearray(R)
+    for _ in range(int(len(V) * rate)):
+        V[rng.randrange(len(V))] = R[rng.randrange(len(R))]
+    return bytes(V)
+
+
+def _pairs(seed):
+    rng = random.Random(seed)
+    out = []
+    for period in (17, 33, 64, 100, 250, 500, 1000):
+        R = _periodic(rng, 65536 + rng.randrange(4096), period)
+        out.append((f"periodic{period}", R, _edit(rng, R, rng.choice([0.002, 0.02, 0.1]))))
+    for k in (2, 3, 4):
+        R = bytes(rng.randrange(k) + 65 for _ in range(40000))
+        for rate in (0.01, 0.05, 0.2):
+            out.append((f"alphabet{k}_{rate}", R, _edit(rng, R, rate)))
+    R = rng.randbytes(50000)
+    # a block of V repeated from elsewhere in R at a short distance
+    V = bytearray(_edit(rng, R, 0.05))
+    for _ in range(20):
+        a = rng.randrange(len(V) - 600)
+        d = rng.randrange(1, 300)
+        V[a:a + 200] = R[a + d:a + d + 200]
+    out.append(("shifted_blocks", R, bytes(V)))
+    return out
+
+
+@pytest.mark.parametrize("q", [1, 7, 97])
+def test_members_adversarial(dg, ctx_mode, orc, q):
+    pairs = _pairs(100 + q)
+    got = dg.encode_batch([(R, V) for _, R, V in pairs], "onepass", p=16, q=q, ctx=ctx_mode)
+    for (name, R, V), d in zip(pairs, got):
+        assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
