@@ -745,7 +745,10 @@ __device__ __forceinline__ void put_bulk(P dst, bool valid, uint32_t my, uint32_
 }
 
 constexpr uint32_t kMemSerStage = 4096;
-constexpr uint32_t kSerWavesPerCu = 16;
+#ifndef DG_MSER_WAVES
+#define DG_MSER_WAVES 16
+#endif
+constexpr uint32_t kSerWavesPerCu = DG_MSER_WAVES;   // persistent serialiser waves per CU (LDS allows 24)
 
 // one job's inputs, loaded a job ahead (descriptors wave-uniform)
 struct SerFetch {
