@@ -297,15 +297,16 @@ int dg_decode_batch_device(dg_context_t *ctx, const uint8_t *d_ref,
                            uint64_t *d_out_len, int32_t *d_status,
                            void *stream);
 
-/* Plan form of the batched decode (C5): descriptors uploaded and CRC
- * segmentation planned once; dg_decode_plan_run is asynchronous device work
- * only (no host synchronisation, graph-capturable).  The reference CRCs run
- * on a plan-owned side stream joined before the verify step; the output CRC
- * spans take their lengths from the delta headers on the device.  Status
- * precedence per stream: DG_ERR_MALFORMED / DG_ERR_CAPACITY, then
- * DG_ERR_SRC_CRC, then DG_ERR_DST_CRC (main.c:335-385).  Arena base pointers
- * d_ref and d_out must be 16-byte aligned.  Timing as for the encode plan;
- * stage names "ref_crc", "decode", "out_crc+verify", "total". */
+/* Plan form of the batched decode (C5): descriptors uploaded once;
+ * dg_decode_plan_run is one kernel launch (no host synchronisation,
+ * graph-capturable) that parses and applies every stream and then computes
+ * the CRC-64/XZ of its reference and of its output (length from the delta
+ * header) and checks both against the header.  Status precedence per
+ * stream: DG_ERR_MALFORMED / DG_ERR_CAPACITY, then DG_ERR_SRC_CRC, then
+ * DG_ERR_DST_CRC (main.c:335-385).  Arena base pointers d_ref and d_out must
+ * be 16-byte aligned.  Timing as for the encode plan; stage names "ref_crc",
+ * "decode", "out_crc+verify", "total" ("decode" covers the CRC checks, the
+ * two CRC stages are empty). */
 typedef struct dg_decode_plan dg_decode_plan_t;
 int dg_decode_plan_create(dg_context_t *ctx, const dg_decode_desc_t *descs,
                           uint32_t n, int ignore_hash,
