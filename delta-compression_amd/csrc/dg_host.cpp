@@ -1013,8 +1013,12 @@ void dg_encode_plan_destroy(dg_encode_plan_t* P) {
 	if (!P) return;
 	hipSetDevice(P->ctx->device);
 	hipStreamSynchronize(P->ctx->stream);
+	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
+	if (P->ev_fork) hipEventDestroy(P->ev_fork);
+	if (P->ev_join) hipEventDestroy(P->ev_join);
+	if (P->side) hipStreamDestroy(P->side);
 	delete P;
 }
 
