@@ -279,6 +279,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
              else "member_chunk_kernel" if members
              else "onepass16_kernel" if aligned16 else "onepass_kernel")
     traffic, traffic_src = pmc_traffic(name, kname) if npg == CONFIGS[name][0] else (None, None)
+    # the path-level roofline of SURVEY §8(d) / BASELINE.md §3: every input
+    # byte read once plus every delta byte written, over the whole step
+    path_bytes = in_bytes_rank + delta_bytes
+    step_s = elapsed / args.steps
     line = {
         "metric": "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X",
         "value": round(value, 3),
@@ -331,9 +335,18 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
                        "them, back to back), mean over the timed steps"),
             "crc_ms_per_step": round(stages.get("crc64", 0.0), 4),
             "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+            "path_bytes_per_step": path_bytes,
+            "path_bytes": "sum(|R|+|V|) + sum|delta| per rank (SURVEY 8(d))",
+            "path_achieved": round(path_bytes / step_s / 1e9, 2),
+            "path_frac": round(path_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5),
         },
         "cpu_baseline": None,
     }
+    if algo == "correcting" and stages.get("corr_build") is not None:
+        # the build and the scan apart (HIP events on the run stream; the
+        # CRC shares the CUs with them)
+        line["roofline"]["kernels_ms"] = {"build": round(stages["corr_build"], 4),
+                                          "scan": round(stages["corr_scan"], 4)}
     plan.close()
     del ref, ver, out, offs, status, sizes, gather
     torch.cuda.empty_cache()
@@ -406,13 +419,16 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     v_bytes = sum(vl for _, _, _, vl in layout)
     d_bytes = d_offs[-1]
     dec_ms = stages.get("decode", 0.0)
-    # decode_kernel algorithmic bytes: the deltas read, the initial R image
-    # written, COPY sources read and the outputs written (in place: the
-    # output buffer starts as R), then R and the output read again by the
-    # in-kernel CRC-64/XZ checks -> |delta| + 2 |R| + 3 |V|
+    # decode algorithmic bytes: every delta byte read, R read
+    # once, the output written once -> |delta| + |R| + |V|.  The kernel as
+    # designed moves more (design_bytes: the in-place image is R copied into
+    # the output first, the COPY sources are read from it, and R and the
+    # output are read again by the in-kernel CRC checks: |delta| + 2|R| + 3|V|)
     r_bytes = sum(rl for _, rl, _, _ in layout)
-    alg = d_bytes + 2 * r_bytes + 3 * v_bytes
+    alg = d_bytes + r_bytes + v_bytes
+    design = d_bytes + 2 * r_bytes + 3 * v_bytes
     achieved = alg / (dec_ms / 1e3) / 1e9 if dec_ms > 0 else 0.0
+    step_s = elapsed / args.steps
     traffic, traffic_src = pmc_traffic(name, "decode_kernel") if npg == CONFIGS[name][0] else (None, None)
     line = {
         "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
@@ -430,9 +446,15 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": alg,
-                     "algorithmic_bytes_per_stream": "|delta| + 2 |R| + 3 |V| (parse + apply + src/dst CRC in one kernel)",
+                     "algorithmic_bytes_per_stream": "|delta| + |R| + |V| (SURVEY 8(d))",
+                     "design_bytes_per_launch": design,
+                     "design_bytes_per_stream": "|delta| + 2 |R| + 3 |V| (R image, COPY sources, "
+                                                "output, both CRC re-reads)",
                      "avg_launch_ms": round(dec_ms, 4),
-                     "stage_ms": {k: round(v, 4) for k, v in stages.items()}},
+                     "stage_ms": {k: round(v, 4) for k, v in stages.items()},
+                     "path_bytes_per_step": alg,
+                     "path_achieved": round(alg / step_s / 1e9, 2),
+                     "path_frac": round(alg / step_s / 1e9 / HBM_PEAK_GBS, 5)},
         "cpu_baseline": None,
     }
     plan.close()

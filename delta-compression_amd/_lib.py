@@ -31,7 +31,7 @@ _ALGOS = {"greedy": ALGO_GREEDY, "onepass": ALGO_ONEPASS, "correcting": ALGO_COR
 STATUS = {
     0: "DG_OK", 1: "DG_ERR_INVALID_ARG", 2: "DG_ERR_UNSUPPORTED", 3: "DG_ERR_TOO_LARGE",
     4: "DG_ERR_NO_DEVICE", 5: "DG_ERR_HIP", 6: "DG_ERR_NOMEM", 7: "DG_ERR_CAPACITY",
-    8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC", 11: "DG_ERR_TABLE_POOL",
+    8: "DG_ERR_MALFORMED", 9: "DG_ERR_SRC_CRC", 10: "DG_ERR_DST_CRC", 11: "DG_ERR_TABLE_POOL", 12: "DG_ERR_INTERNAL",
 }
 LIMIT_TABLE_POOL_BYTES = 0
 LIMIT_ONEPASS_MEMBERS = 1
@@ -626,8 +626,13 @@ def encode_delta(commands: list, *, inplace: bool = False, version_size: int, sr
 
 
 def decode_delta(data: bytes):
-    """delta.py:967-999: (commands, inplace, version_size, src_crc, dst_crc)
-    via dg_delta_decode; a malformed stream raises DeltaError (code 8)."""
+    """delta.py:967-999's name and return value (commands, inplace,
+    version_size, src_crc, dst_crc), via dg_delta_decode.  Malformed input
+    follows the C decoder (encoding.c:111-178), not delta.py: an unknown
+    command type or a COPY/ADD cut short by the buffer end raises
+    DeltaError (code 8) where delta.py skips unknown types and returns
+    truncated ADD data.  tests/test_format_cpu.py::test_decode_errors pins
+    this choice."""
     cl, hdr = Commands(), DeltaInfo()
     rc = lib.dg_delta_decode(_u8(data), len(data), C.byref(cl), C.byref(hdr))
     if rc:

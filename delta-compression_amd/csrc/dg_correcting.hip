@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 	int32_t st = 0;
 
 	// the oldest buffer entry leaves for the output when the buffer is full
-	// (correcting.c:603-613)
+	// (correcting.c:319-330, 343-350, 421-428)
 	auto emit_oldest_if_full = [&]() {
 		if (n >= bc) {
 			const RingEnt o = ring[head];
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 // pairs with larger indexes take the memory-atomic build (their tables must
 // have been cleared to ~0 by the caller).  qmin/qmax: index sizes in the batch.
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap,
-                             uint64_t qmin) {
+                             uint64_t qmin, hipEvent_t ev_built) {
 	(void)p;
 	if (a.n_pairs == 0) return hipSuccess;
 	hipLaunchKernelGGL(correcting_class_kernel, dim3((a.n_pairs + 63) / 64), dim3(64), 0, st, a);
@@ -616,6 +616,10 @@ hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, ui
 		hipLaunchKernelGGL(correcting_build_kernel, dim3((uint32_t)blocks), dim3(kBuildBlock), 0, st, a, nchunk, lds_cap);
 	}
 	if (a.stats) hipLaunchKernelGGL(correcting_stats_kernel, dim3(a.n_pairs), dim3(256), 0, st, a);
+	if (ev_built) {
+		const hipError_t e = hipEventRecord(ev_built, st);
+		if (e != hipSuccess) return e;
+	}
 	const size_t lds = sizeof(RingEnt) * ((size_t)(a.buf_cap ? a.buf_cap : 1) + 1);
 	hipLaunchKernelGGL(correcting_scan_kernel, dim3(a.n_pairs), dim3(64), lds, st, a);
 	return hipGetLastError();

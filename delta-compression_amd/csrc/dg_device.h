@@ -230,6 +230,7 @@ struct SynthCopy {   // V[dst..+len) = R[src..+len)
 const char* ab_env(const char* name);
 // the context's slot for the pipelined host path's state, and its destructor
 void** ctx_io(dg_context_t* ctx, void (*release)(void*));
+uint64_t ctx_limits_gen(const dg_context_t* ctx);   // changes with every dg_context_set_limit
 // --verbose: the reference's diagnostic lines for pair i of a plan to stderr,
 // from the plan's parameters, its 8 device counters (copied to the host; may
 // be NULL for onepass) and the pair's delta (dg_host.cpp)
@@ -241,7 +242,9 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
-hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin);
+// ev_built (nullable): recorded after the R-index build, before the V scan (stage timing)
+hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
+                             hipEvent_t ev_built);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after

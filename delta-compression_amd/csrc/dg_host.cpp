@@ -110,6 +110,7 @@ struct dg_context {
 	uint32_t n_cu = 256;                // compute units (grid caps)
 	uint64_t table_pool_bytes = 0;      // DG_LIMIT_TABLE_POOL_BYTES (0 = automatic)
 	uint64_t onepass_members = 0;       // DG_LIMIT_ONEPASS_MEMBERS (0 auto, 1 on, 2 off)
+	uint64_t limits_gen = 0;            // bumped by every dg_context_set_limit (cached plans key on it)
 	std::string err;
 	// scratch reused by the host-buffer entry points
 	void* pin = nullptr;
@@ -117,6 +118,8 @@ struct dg_context {
 	void* io = nullptr;                 // dg_encode_pipelined's slots (dg_host_io.cpp)
 	void (*io_free)(void*) = nullptr;
 };
+
+uint64_t dg::ctx_limits_gen(const dg_context_t* ctx) { return ctx->limits_gen; }
 
 void** dg::ctx_io(dg_context_t* ctx, void (*release)(void*)) {
 	ctx->io_free = release;
@@ -169,6 +172,7 @@ const char* dg_status_string(int s) {
 	case DG_ERR_SRC_CRC: return "source file does not match delta";
 	case DG_ERR_DST_CRC: return "output integrity check failed";
 	case DG_ERR_TABLE_POOL: return "onepass work-table pool exhausted";
+	case DG_ERR_INTERNAL: return "internal invariant failed on the device (library bug)";
 	default: return "unknown status";
 	}
 }
@@ -259,10 +263,14 @@ void* dg_context_stream(dg_context_t* ctx) { return ctx ? (void*)ctx->stream : n
 int dg_context_set_limit(dg_context_t* ctx, int limit, uint64_t value) {
 	if (!ctx) return DG_ERR_INVALID_ARG;
 	switch (limit) {
-	case DG_LIMIT_TABLE_POOL_BYTES: ctx->table_pool_bytes = value; return DG_OK;
+	case DG_LIMIT_TABLE_POOL_BYTES:
+		ctx->table_pool_bytes = value;
+		++ctx->limits_gen;
+		return DG_OK;
 	case DG_LIMIT_ONEPASS_MEMBERS:
 		if (value > 2) return set_err(ctx, DG_ERR_INVALID_ARG, "onepass members mode %llu", (unsigned long long)value);
 		ctx->onepass_members = value;
+		++ctx->limits_gen;
 		return DG_OK;
 	default: return set_err(ctx, DG_ERR_INVALID_ARG, "unknown limit %d", limit);
 	}
@@ -310,6 +318,11 @@ struct DevBuf {
 	void* p = nullptr;
 	size_t n = 0;
 	~DevBuf() { if (p) hipFree(p); }
+	void release() {
+		if (p) hipFree(p);
+		p = nullptr;
+		n = 0;
+	}
 	int alloc(size_t bytes) {
 		if (p) { hipFree(p); p = nullptr; }
 		n = bytes;
@@ -366,7 +379,7 @@ struct dg_encode_plan {
 	hipEvent_t* cur = nullptr;   // event set of the run being enqueued
 };
 
-static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total", "members"};
+static const char* kStageNames[] = {"crc64", "diff", "scan", "serialize+join", "total", "members", "corr_build", "corr_scan"};
 
 // ── --verbose: the reference's diagnostics from device counters and the delta ──
 
@@ -680,17 +693,30 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			slots += (uint64_t)nch * kMemChunkSlots;
 			P->n_chunks += nch;
 		}
-		bad |= P->d_mem_s.alloc(4ull * std::max<uint64_t>(slots, 1));
-		bad |= P->d_srec.alloc(16ull * std::max<uint64_t>(slots, 1));
-		bad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(P->n_chunks, 1));
-		bad |= P->d_chunks.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
-		bad |= P->d_csum.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
-		bad |= P->d_cmap.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
-		bad |= P->d_seg.alloc(16ull * ((uint64_t)P->n_chunks + 2ull * n));
-		bad |= P->d_nseg.alloc(4ull * std::max<uint32_t>(n, 1));
-		if (!bad && !jobs.empty() &&
+		int mbad = 0;
+		mbad |= P->d_mem_s.alloc(4ull * std::max<uint64_t>(slots, 1));
+		mbad |= P->d_srec.alloc(16ull * std::max<uint64_t>(slots, 1));
+		mbad |= P->d_nmem.alloc(4ull * std::max<uint32_t>(P->n_chunks, 1));
+		mbad |= P->d_chunks.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		mbad |= P->d_csum.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		mbad |= P->d_cmap.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
+		mbad |= P->d_seg.alloc(16ull * ((uint64_t)P->n_chunks + 2ull * n));
+		mbad |= P->d_nseg.alloc(4ull * std::max<uint32_t>(n, 1));
+		if (!mbad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
-			bad = 1;
+			mbad = 1;
+		if (mbad && ctx->onepass_members != 1) {
+			// automatic mode: member mode is an optimisation, so a batch that
+			// fits with the plain chain still gets a plan
+			(void)hipGetLastError();
+			for (DevBuf* b : {&P->d_mem_s, &P->d_srec, &P->d_nmem, &P->d_chunks, &P->d_csum, &P->d_cmap,
+			                  &P->d_seg, &P->d_nseg})
+				b->release();
+			P->members = false;
+			P->n_chunks = 0;
+			mbad = 0;
+		}
+		bad |= mbad;
 	}
 	if (bad) {
 		delete P;
@@ -775,7 +801,7 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 	return P ? P->d_nrec.as<uint32_t>() : nullptr;
 }
 
-constexpr int kTimingEvents = 7;
+constexpr int kTimingEvents = 8;
 
 int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
@@ -798,24 +824,27 @@ int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 // Per-run events: 0/1 around the CRC kernels (side stream), 2/3 around the
 // differencing kernel(s), 4 after the scan, 5 after serialisation + the CRC
 // join + the header patch (DG_SER_BLOCK=1 / DG_FUSED=1: the join falls before
-// 4), 6 after the member kernel (member mode; else with 2).
+// 4), 6 after the member kernel (member mode; else with 2), 7 after the
+// correcting R-index build (before the V scan; onepass: with 3).  Stages
+// corr_build (2..7) and corr_scan (7..3) are reported for correcting plans only.
 // Returns the mean over the runs recorded since set_timing (at most `slots`).
 int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
 	if (!P || !P->slots || !P->runs) return 0;
 	const uint32_t used = std::min(P->runs, P->slots);
-	const int pairs[6][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}, {2, 6}};
-	double acc[6] = {};
+	const int pairs[8][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}, {2, 6}, {2, 7}, {7, 3}};
+	const int ns = P->algo == DG_ALGO_CORRECTING ? 8 : 6;
+	double acc[8] = {};
 	for (uint32_t s = 0; s < used; ++s) {
 		hipEvent_t* e = &P->ev[(size_t)kTimingEvents * s];
 		if (hipEventSynchronize(e[5]) != hipSuccess) return 0;
-		for (int k = 0; k < 6; ++k) {
+		for (int k = 0; k < ns; ++k) {
 			float t = 0;
 			hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]);
 			acc[k] += t;
 		}
 	}
 	int k = 0;
-	for (; k < 6 && k < n; ++k) {
+	for (; k < ns && k < n; ++k) {
 		if (ms) ms[k] = (float)(acc[k] / used);
 		if (names) names[k] = kStageNames[k];
 	}
@@ -927,8 +956,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// the LDS build writes every slot of every index; the global
 			// build only fills, so its tables start empty (~0)
 			if (P->qmax > P->corr_lds_cap) HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
-			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin));
+			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin,
+			                              P->timing ? P->cur[7] : nullptr));
 		}
+		if (P->timing && P->algo != DG_ALGO_CORRECTING) HIPCHK(ctx, hipEventRecord(P->cur[7], st));
 		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[3], st));
 		return DG_OK;
 	};
@@ -1070,6 +1101,8 @@ struct dg_decode_plan {
 	uint32_t n = 0;
 	int ignore_hash = 0;
 	DevBuf d_desc;   // the decode kernel computes and checks both CRCs itself
+	// byte extents the streams touch in each arena (run rejects overlaps)
+	uint64_t ref_end = 0, delta_end = 0, out_end = 0;
 	bool timing = false;
 	std::vector<hipEvent_t> ev;
 	uint32_t slots = 0, runs = 0;
@@ -1097,6 +1130,11 @@ int dg_decode_plan_create(dg_context_t* ctx, const dg_decode_desc_t* descs, uint
 			delete P;
 			return set_err(ctx, DG_ERR_TOO_LARGE, "stream %u exceeds the u32 format", i);
 		}
+	for (uint32_t i = 0; i < n; ++i) {
+		P->ref_end = std::max(P->ref_end, descs[i].ref_off + descs[i].ref_len);
+		P->delta_end = std::max(P->delta_end, descs[i].delta_off + descs[i].delta_len);
+		P->out_end = std::max(P->out_end, descs[i].out_off + descs[i].out_cap);
+	}
 	const size_t nn = std::max<size_t>(n, 1);
 	if (P->d_desc.alloc(sizeof(dg_decode_desc_t) * nn)) {
 		delete P;
@@ -1165,6 +1203,17 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		return set_err(ctx, DG_ERR_INVALID_ARG, "null device buffer");
 	if (((uintptr_t)d_ref & 15) || ((uintptr_t)d_out & 15))
 		return set_err(ctx, DG_ERR_INVALID_ARG, "arena base pointers must be 16-byte aligned");
+	{
+		// the kernel writes the output image before it reads R for the source
+		// CRC, and reads the delta while it writes: an output arena that
+		// overlaps the reference or delta bytes of the batch is rejected
+		auto overlap = [](const void* a, uint64_t na, const void* b, uint64_t nb) {
+			const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+			return na && nb && x < y + nb && y < x + na;
+		};
+		if (overlap(d_out, P->out_end, d_ref, P->ref_end) || overlap(d_out, P->out_end, d_delta, P->delta_end))
+			return set_err(ctx, DG_ERR_INVALID_ARG, "the output arena overlaps the reference or delta arena");
+	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
 	hipEvent_t* ev = nullptr;
 	if (P->timing) ev = &P->ev[(size_t)kDecEvents * (P->runs++ % P->slots)];

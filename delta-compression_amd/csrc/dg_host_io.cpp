@@ -187,6 +187,7 @@ struct IoSlot {
 	std::vector<dg_pair_t> key;   // the plan's layout (chunk-relative)
 	dg_algorithm_t key_algo = DG_ALGO_ONEPASS;
 	dg_diff_options_t key_opts{};
+	uint64_t key_limits = ~0ull;  // dg::ctx_limits_gen when the plan was made
 	Dev d_ref, d_ver, d_out, d_off, d_st;
 	uint64_t cap_ref = 0, cap_ver = 0, cap_out = 0, cap_doff = 0, cap_dst = 0;
 	Pinned h_in, h_out, h_off, h_st;
@@ -226,6 +227,35 @@ void par_memcpy(void* dst, const void* src, uint64_t n) {
 		if (a < b) th.emplace_back([=] { memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
 	}
 	memcpy(dst, src, std::min(n, per));
+	for (auto& x : th) x.join();
+}
+
+// pageable -> pinned staging of a chunk's pairs at their packed (16-byte
+// aligned) offsets `rel`, the pairs split over a few host threads
+void stage_pairs(uint8_t* dr, uint8_t* dv, const uint8_t* h_ref, const uint8_t* h_ver, const dg_pair_t* src,
+                 const dg_pair_t* rel, uint32_t m) {
+	auto run = [&](uint32_t a, uint32_t b) {
+		for (uint32_t i = a; i < b; ++i) {
+			memcpy(dr + rel[i].r_off, h_ref + src[i].r_off, src[i].r_len);
+			memcpy(dv + rel[i].v_off, h_ver + src[i].v_off, src[i].v_len);
+		}
+	};
+	uint64_t bytes = 0;
+	for (uint32_t i = 0; i < m; ++i) bytes += src[i].r_len + src[i].v_len;
+	unsigned t = std::thread::hardware_concurrency();
+	t = std::max(1u, std::min(8u, t));
+	const uint64_t parts = std::min<uint64_t>({t, m, std::max<uint64_t>(1, bytes >> 23)});
+	if (parts <= 1) {
+		run(0, m);
+		return;
+	}
+	std::vector<std::thread> th;
+	const uint32_t per = (uint32_t)((m + parts - 1) / parts);
+	for (uint64_t k = 1; k < parts; ++k) {
+		const uint32_t a = (uint32_t)(k * per), b = std::min<uint32_t>(m, a + per);
+		if (a < b) th.emplace_back([=] { run(a, b); });
+	}
+	run(0, std::min<uint32_t>(m, per));
 	for (auto& x : th) x.join();
 }
 
@@ -305,7 +335,13 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 		const int32_t* st = sl.h_st.as<int32_t>();
 		const uint64_t total = off[m];
 		if (full || out_pos + total > out_cap) {
+			// this chunk and every later one do not fit: their offsets stay
+			// at the bytes written so far, their status says why
 			full = true;
+			for (uint32_t k = 0; k < m; ++k) {
+				out_offsets[sl.p0 + k + 1] = out_pos;
+				if (status) status[sl.p0 + k] = DG_ERR_CAPACITY;
+			}
 			return DG_OK;
 		}
 		if (total) {
@@ -345,15 +381,31 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 			v_lo = std::min<uint64_t>(v_lo, pairs[i].v_off);
 			v_hi = std::max<uint64_t>(v_hi, pairs[i].v_off + pairs[i].v_len);
 		}
-		// keep the arena's 16-byte phase so aligned layouts stay aligned
+		// pinned arenas go up in one copy per stream and keep the arena's
+		// 16-byte phase (aligned layouts stay aligned); pageable arenas are
+		// staged pair by pair anyway, so the staging copy packs every stream
+		// at a 16-byte offset, which selects the LDS-window kernels
 		r_lo &= ~15ull;
 		v_lo &= ~15ull;
-		const uint64_t rn = r_hi - r_lo, vn = v_hi - v_lo;
+		uint64_t rn = r_hi - r_lo, vn = v_hi - v_lo;
 		rel.resize(m);
-		for (uint32_t i = p0; i < p1; ++i)
-			rel[i - p0] = dg_pair_t{pairs[i].r_off - r_lo, pairs[i].r_len, pairs[i].v_off - v_lo, pairs[i].v_len};
+		if (in_pinned) {
+			for (uint32_t i = p0; i < p1; ++i)
+				rel[i - p0] = dg_pair_t{pairs[i].r_off - r_lo, pairs[i].r_len, pairs[i].v_off - v_lo, pairs[i].v_len};
+		} else {
+			uint64_t ro = 0, vo = 0;
+			for (uint32_t i = p0; i < p1; ++i) {
+				rel[i - p0] = dg_pair_t{ro, pairs[i].r_len, vo, pairs[i].v_len};
+				ro += (pairs[i].r_len + 15) & ~15ull;
+				vo += (pairs[i].v_len + 15) & ~15ull;
+			}
+			rn = ro;
+			vn = vo;
+		}
+		const uint64_t lim = dg::ctx_limits_gen(ctx);
 		const bool same = sl.plan && sl.key_algo == algo && !memcmp(&sl.key_opts, &o, sizeof o) &&
-		                  sl.key.size() == rel.size() && !memcmp(sl.key.data(), rel.data(), m * sizeof(dg_pair_t));
+		                  sl.key_limits == lim && sl.key.size() == rel.size() &&
+		                  !memcmp(sl.key.data(), rel.data(), m * sizeof(dg_pair_t));
 		if (!same) {
 			if (sl.plan) dg_encode_plan_destroy(sl.plan);
 			sl.plan = nullptr;
@@ -361,6 +413,7 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 			sl.key = rel;
 			sl.key_algo = algo;
 			sl.key_opts = o;
+			sl.key_limits = lim;
 			sl.bound = dg_encode_plan_output_bound(sl.plan);
 		}
 		if (!grow(sl.d_ref, sl.cap_ref, rn) || !grow(sl.d_ver, sl.cap_ver, vn) ||
@@ -372,10 +425,9 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 		}
 		const uint8_t* src_r = h_ref + r_lo;
 		const uint8_t* src_v = h_ver + v_lo;
-		if (!in_pinned) {   // stage: one host copy per stream per chunk
+		if (!in_pinned) {   // stage: every pair's streams at 16-byte offsets
 			if (!grow(sl.h_in, sl.cap_hin, rn + vn)) { rc = DG_ERR_NOMEM; break; }
-			par_memcpy(sl.h_in.p, src_r, rn);
-			par_memcpy(sl.h_in.as<uint8_t>() + rn, src_v, vn);
+			stage_pairs(sl.h_in.as<uint8_t>(), sl.h_in.as<uint8_t>() + rn, h_ref, h_ver, pairs + p0, rel.data(), m);
 			src_r = sl.h_in.as<uint8_t>();
 			src_v = src_r + rn;
 		}
@@ -490,7 +542,9 @@ void transpose_layout(uint64_t seed, uint32_t nb, uint32_t mean, uint32_t pct,
 	perm.resize(nb);
 	std::vector<uint32_t> idx(nb), val(nb);
 	for (uint32_t i = 0; i < nb; ++i) perm[i] = idx[i] = i;
-	const uint32_t kk = (uint32_t)(((uint64_t)nb * pct + 50) / 100);
+	// Python's round() is round-half-to-even (gen_transpositions.py:143)
+	const uint64_t kq = (uint64_t)nb * pct / 100, kr = (uint64_t)nb * pct % 100;
+	const uint32_t kk = (uint32_t)(kq + (kr > 50 || (kr == 50 && (kq & 1))));
 	if (kk < 2) return;
 	for (uint32_t j = 0; j < kk; ++j) {
 		const uint32_t t = j + (uint32_t)(splitmix_at_host(s, k++) % (nb - j));

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
 	}
 	if (tid == 0) {
 		out[pos] = 0;   // END
-		if (pos + 1 != end - base) s.status[pair] = 5;   // size pass disagreed
+		if (pos + 1 != end - base) s.status[pair] = 12;   // DG_ERR_INTERNAL: size pass disagreed
 	}
 }
 

@@ -869,7 +869,7 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 					uint8_t* o = out + e.z;
 					if (e.x == kSegTail) {
 						const uint64_t n = put_tail(o, V, vl, e.w);
-						if (e.z + n != F.end - F.base && lane == 0) a.status[F.J.pair] = 5;   // sizes disagree
+						if (e.z + n != F.end - F.base && lane == 0) a.status[F.J.pair] = 12;   // DG_ERR_INTERNAL: sizes disagree
 					} else {
 						const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (F.J.rec_base + e.x), kRecWordsOnepass};
 						serialize_run<kMemSerStage, 1>(o, V, vl, src, e.y, e.w, (sw_lds8*)stage);

@@ -131,6 +131,7 @@ __device__ __forceinline__ uint32_t mask_transpose_8x4(uint32_t x) {
 // table before its pair fails with DG_ERR_TABLE_POOL.
 constexpr uint64_t kTableWaitTicks = 20ull * 100000000ull;   // 20 s
 constexpr int32_t kStatusTablePool = 11;                     // DG_ERR_TABLE_POOL
+constexpr int32_t kStatusInternal = 12;                      // DG_ERR_INTERNAL
 
 __device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
 	return ((unsigned long long)tag << 32) | (0xFFFFFFFFu - rel);
@@ -744,7 +745,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			if (nseg < seg_cap) {
 				if (lane == 0) *(uint4*)(sgp + 4ull * nseg) = make_uint4(nb_first, nrec - nb_first, nb_boff, nb_prev);
 			} else {
-				st = 5;
+				st = kStatusInternal;
 			}
 			++nseg;
 		}
@@ -811,7 +812,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		// the chain always ends on an unverified member (the final epoch's
 		// run holds the end of the shorter stream)
 		mem_live = kc < nch;
-		if (!mem_live) { st = 5; scanning = false; return; }
+		if (!mem_live) { st = kStatusInternal; scanning = false; return; }
 		s_cur = uni(msp[(uint64_t)kc * kMemChunkSlots + ki]);
 		v0 = r0 = s_cur;
 		at_mismatch = kc != 0 || ki != 0;   // member starts past the first are mismatches
@@ -1127,7 +1128,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		if (nseg < seg_cap) {
 			if (lane == 0) *(uint4*)(sgp + 4ull * nseg) = make_uint4(kSegTail, 0u, (uint32_t)(dsz - 1), v0);
 		} else {
-			st = 5;
+			st = kStatusInternal;
 		}
 		++nseg;
 		if (lane == 0) a.nseg[pair] = nseg;

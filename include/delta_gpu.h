@@ -69,9 +69,12 @@ typedef enum {
 	DG_ERR_MALFORMED   = 8,   /* not a delta / truncated / bad command */
 	DG_ERR_SRC_CRC     = 9,   /* reference does not match src_crc */
 	DG_ERR_DST_CRC     = 10,  /* reconstructed output does not match dst_crc */
-	DG_ERR_TABLE_POOL  = 11   /* onepass: no work table came free within the
+	DG_ERR_TABLE_POOL  = 11,  /* onepass: no work table came free within the
 	                             wait bound (more long-epoch pairs in flight than
 	                             tables; raise DG_LIMIT_TABLE_POOL_BYTES) */
+	DG_ERR_INTERNAL    = 12   /* a device-side invariant failed (a library bug:
+	                             segment list overflow, a member chain that ran
+	                             out of members, serialiser size disagreement) */
 } dg_status_t;
 
 /* Numbering matches delta_algorithm_t (src/c/delta.h:85). */
@@ -139,7 +142,11 @@ int dg_abi_version(void);
 /*   DG_LIMIT_ONEPASS_MEMBERS: how onepass plans (seed length 16, 16-byte
  *     aligned pairs) run the epoch chain.  0 = automatic, 1 = verified
  *     diagonal members first (the chain walks only unverified members), 2 =
- *     the plain per-pair chain.  Output bytes are identical in every mode. */
+ *     the plain per-pair chain.  Output bytes are identical in every mode.
+ *     Member mode needs about 1.3 B of extra device memory per position of
+ *     min(|R|, |V|) (20 B for each of 129 member slots per 2 KiB chunk); when
+ *     that allocation fails in automatic mode the plan falls back to the
+ *     plain chain, and only a forced mode 1 returns DG_ERR_NOMEM. */
 #define DG_LIMIT_ONEPASS_MEMBERS 1
 int dg_context_set_limit(dg_context_t *ctx, int limit, uint64_t value);
 
@@ -237,12 +244,16 @@ int dg_encode_batch(dg_context_t *ctx, dg_algorithm_t algo,
  * chunk i.  The deltas land in h_out (out_cap bytes) packed in pair order,
  * delta i at out_offsets[i] .. out_offsets[i+1] (host, n+1 entries); status[i]
  * per pair (host, may be NULL).  Arenas and h_out from dg_host_alloc (pinned)
- * are copied directly; other host memory goes through pinned staging that
- * the context keeps between calls, as are the device buffers and plans (a
- * chunk with the same layout as the slot's last one reuses its plan).
+ * are copied directly (keeping the arena's 16-byte phase); other host memory
+ * goes through pinned staging that the context keeps between calls, which
+ * places every pair's streams at 16-byte offsets on the device (so unaligned
+ * pageable layouts still take the LDS-window kernels).  Device buffers and
+ * plans are kept too: a chunk with the same layout, options and context
+ * limits as the slot's last one reuses its plan.
  * Returns DG_OK (per-pair failures in status), DG_ERR_CAPACITY when h_out is
- * too small (out_offsets then hold the bytes written so far), or the first
- * failure when status is NULL. */
+ * too small (the pairs that did not fit get status DG_ERR_CAPACITY and
+ * out_offsets equal to the bytes written so far), or the first failure when
+ * status is NULL. */
 int dg_encode_pipelined(dg_context_t *ctx, dg_algorithm_t algo,
                         const uint8_t *h_ref, const uint8_t *h_ver,
                         const dg_pair_t *pairs, uint32_t n_pairs,
@@ -283,7 +294,12 @@ int dg_decode(dg_context_t *ctx, const uint8_t *r, size_t r_len,
 /* Batched device decode: stream i is d_delta[delta_off[i] .. +delta_len[i])
  * applied to d_ref[ref spans i]; output written to d_out at out_off[i]
  * (capacity out_cap[i] >= version_size, and >= |R| for in-place deltas).
- * d_status[i] receives a dg_status_t. Descriptors are host arrays. */
+ * d_status[i] receives a dg_status_t. Descriptors are host arrays.  The
+ * output bytes the descriptors name must not overlap the reference or delta
+ * bytes they name (the in-place replay runs in the output buffer after R is
+ * copied into it, and the source CRC is computed from d_ref after the
+ * apply): an overlapping call returns DG_ERR_INVALID_ARG and writes nothing.
+ * The output is written even when a stream's source CRC check fails. */
 typedef struct {
 	uint64_t ref_off, ref_len;
 	uint64_t delta_off, delta_len;

@@ -598,7 +598,10 @@ size_t or_synth_transpose(uint64_t seed, uint32_t nb, uint32_t mean,
 	for (uint32_t i = 0; i < nb; i++) off[i + 1] = off[i] + sz[i];
 	size_t total = off[nb];
 	if (total > cap) total = 0;
-	uint32_t kk = (uint32_t)(((uint64_t)nb * pct + 50) / 100);
+	/* k = round(n * perm_pct / 100) with Python's round-half-to-even
+	 * (gen_transpositions.py:143) */
+	uint64_t kq = (uint64_t)nb * pct / 100, kr = (uint64_t)nb * pct % 100;
+	uint32_t kk = (uint32_t)(kq + (kr > 50 || (kr == 50 && (kq & 1))));
 	for (uint32_t i = 0; i < nb; i++) { perm[i] = i; idx[i] = i; }
 	if (kk >= 2) {
 		for (uint32_t j = 0; j < kk; j++) {   /* choose kk distinct slots */
