@@ -60,11 +60,17 @@ CONFIGS = {
     "c5": (1024, 65536, 0.01, 1, 0xC2000000,
            "1024 in-place deltas of C2 pairs per GPU (device onepass encode + dg_make_inplace "
            "localmin, ~1.1M COPY/ADD commands), decode + src/dst CRC verify on device", "decode"),
+    # stated extra line (not a BASELINE config): in-place
+    # deltas whose COPYs move, so the replay order matters (apply.c:253-267)
+    "c5o": (1024, 262144, -50, 1, 0xC4000000,
+            "1024 in-place deltas of C4 transposition pairs per GPU (device correcting encode + "
+            "dg_make_inplace localmin: moving COPYs, order-dependent replay), decode + src/dst CRC "
+            "verify on device", "decode"),
 }
 # oracle/_ref/ref_bench modes: encode onepass / correcting; decode standard / in-place deltas
-REF_MODE = {"onepass": 1, "correcting": 2, "decode": 12}
+REF_MODE = {"onepass": 1, "correcting": 2, "decode": 12, "decode_correcting": 13}
 # CPU baseline samples (pairs): ~1-3 s per timed repetition of the reference's src/c
-CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096)}
+CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096), "c5o": (128, 1024)}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -130,8 +136,8 @@ def cpu_model() -> str:
 def _ref_bench(cfg, pairs, threads, reps=5):
     npg, L, rate, q, seed, _, algo = cfg
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
-    cmd = [exe, str(REF_MODE[algo]), str(pairs), str(L), str(rate), str(seed), str(threads), str(q),
-           str(reps)]
+    mode = REF_MODE["decode_correcting" if algo == "decode" and rate < 0 else algo]
+    cmd = [exe, str(mode), str(pairs), str(L), str(rate), str(seed), str(threads), str(q), str(reps)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, check=True)
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -154,8 +160,9 @@ def cpu_baseline(name):
         print(f"cpu_baseline failed: {e}", file=sys.stderr)
         return None
     algo = cfg[6]
+    enc = "correcting" if cfg[2] < 0 else "onepass"
     work = ("delta_decode + delta_apply_delta_inplace + src/dst CRC checks of in-place "
-            "(localmin) onepass deltas; rate = sum |V| / time" if algo == "decode" else
+            f"(localmin) {enc} deltas; rate = sum |V| / time" if algo == "decode" else
             f"{algo} chain crc x2 + delta_diff + delta_place_commands + delta_encode; "
             "rate = sum(|R|+|V|) / time")
     return {
@@ -261,9 +268,11 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         if int(gather.offsets[-1].item()) != int(tot.item()):
             raise SystemExit(f"{name}: global output index inconsistent")
 
-    plan.set_timing(args.steps)   # one HIP-event set per timed step, read after the region
+    timing = getattr(args, "stage_timing", "all")
+    if timing != "none":
+        plan.set_timing(args.steps)   # one HIP-event set per timed step, read after the region
     elapsed = timed(R, args, step)
-    stages = plan.stage_times()
+    stages = plan.stage_times() if timing != "none" else {}
     plan.set_timing(0)
     elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
 
@@ -354,11 +363,11 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
 
 
 def bench_decode(name, args, R, dg, ctx, shard, stream):
-    """C5: in-place deltas of this rank's C2-style pairs are produced first
-    (untimed: device onepass encode, then dg_make_inplace(localmin) on the
-    host, as `delta encode --inplace` does); one step = dg_decode_plan_run
-    over all of them (reference CRC on a side stream, decode, output CRC,
-    verify)."""
+    """C5 / C5o: in-place deltas of this rank's pairs are produced first
+    (untimed: device onepass (C2 pairs) or correcting (C4 transposition
+    pairs) encode, then dg_make_inplace(localmin) on the host, as `delta
+    encode --inplace` does); one step = dg_decode_plan_run over all of them
+    (one kernel: parse, apply, source and output CRC-64/XZ checks)."""
     torch = R.torch
     cfg = CONFIGS[name]
     npg, L, rate, q, seed_base, desc, algo = cfg
@@ -369,7 +378,8 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     lo, hi = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")[R.rank]
     n = hi - lo
     ref, ver, layout = make_inputs(dg, ctx, torch, cfg, lo, n, stream)
-    enc = dg.EncodePlan(ctx, "onepass", layout, q=q)
+    enc_algo = "onepass" if rate >= 0 else "correcting"
+    enc = dg.EncodePlan(ctx, enc_algo, layout, q=q)
     d_arena = torch.empty(enc.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     est = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -383,19 +393,28 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     enc.close()
     del d_arena, est
     deltas, commands = [], 0
+    moving = 0
     for i, (r_off, r_len, v_off, v_len) in enumerate(layout):
         d = dg.make_inplace(ref_h[r_off:r_off + r_len], std[o[i]:o[i + 1]], policy="localmin")
         deltas.append(d)
         commands += dg.info(d)["num_commands"]
+        if rate < 0:   # COPYs that move (src != dst): the replay order matters
+            moving += sum(1 for c in dg.decode_delta(d)[0] if isinstance(c, dg.PlacedCopy) and c.src != c.dst)
     del std, ref_h
     d_offs = [0]
     for d in deltas:
         d_offs.append(d_offs[-1] + len(d))
     d_dev = torch.frombuffer(bytearray(b"".join(deltas)), dtype=torch.uint8).to("cuda")
-    descs = [(r_off, r_len, d_offs[i], len(deltas[i]), i * L, max(r_len, v_len))
+    # output i at V's own arena offset (16-byte aligned), room for max(|R|, |V|)
+    descs = [(r_off, r_len, d_offs[i], len(deltas[i]), v_off, max(r_len, v_len))
              for i, (r_off, r_len, v_off, v_len) in enumerate(layout)]
     plan = dg.DecodePlan(ctx, descs)
-    out = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    out_bytes = max(max(d[4] + d[5] for d in descs), ver.numel())
+    out = torch.empty(out_bytes, dtype=torch.uint8, device="cuda")
+    pads = [(v_off + v_len, (v_off + v_len + 15) // 16 * 16) for _, _, v_off, v_len in layout]
+    if any(b > a for a, b in pads):   # the arena's padding between streams is not part of V
+        for a, b in pads:
+            ver[a:b] = 0
     out_len = torch.empty(n, dtype=torch.int64, device="cuda")
     status = torch.empty(n, dtype=torch.int32, device="cuda")
 
@@ -410,7 +429,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     torch.cuda.synchronize()
     step()
     torch.cuda.synchronize()
-    if int(status.abs().sum()) != 0 or not torch.equal(out, ver[:n * L]):
+    if int(status.abs().sum()) != 0 or not torch.equal(out[:ver.numel()], ver):
         raise SystemExit(f"{name}: decode failed: status {status.unique().tolist()}")
     plan.set_timing(args.steps)
     elapsed = timed(R, args, step)
@@ -436,10 +455,13 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
         "unit": "GiB/s", "n_gpus": R.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (C2 pairs generated on device; deltas from the device encoder, "
-                "converted to in-place by dg_make_inplace localmin)",
+        "data": (f"synthetic ({'C2' if rate >= 0 else 'C4 transposition'} pairs generated on device; "
+                 f"deltas from the device {enc_algo} encoder, converted to in-place by "
+                 "dg_make_inplace localmin)"),
         "config": {"workload": desc, "name": name, "inplace": True, "policy": "localmin",
+                   "encoder": enc_algo, "pair_bytes": L,
                    "streams_per_gpu": n, "commands_per_gpu": commands, "delta_bytes_per_gpu": d_bytes,
+                   "moving_copies_per_gpu": moving if rate < 0 else None,
                    "parallelism": f"dp{R.world} (stream shards)"},
         "roofline": {"bound": "hbm", "kernel": "decode_kernel", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -535,7 +557,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--also", default="c3,c4,c5",
+    ap.add_argument("--also", default="c3,c4,c5,c5o",
                     help="extra configs measured in the same run, reported under 'also' "
                          "('none' to skip)")
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")

@@ -383,6 +383,7 @@ __device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len, uint
 // Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
 // and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
 // tables read through the cache, at most 64 VGPRs.
+#ifndef DG_CRC_R1
 __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	__shared__ uint64_t T[4 * 256];
 	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
@@ -398,6 +399,87 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 		if (lane_id() == 0) a.seg_crc[seg] = c;
 	}
 }
+#else
+__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {   // A/B: the round-1 body (DG_CRC_R1)
+	__shared__ uint64_t T[4 * 256];
+	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6;
+	const uint32_t lane = lane_id();
+	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
+	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
+	     seg += gridDim.x * kCrcWavesPerBlock) {
+	const CrcSegDev sd = a.segs[seg];
+	const CrcSpanDev sp = a.spans[sd.span];
+	const uintptr_t start = (uintptr_t)(a.arena[sp.which] + sp.off);
+	const uintptr_t end = start + sp.len;
+	const uintptr_t a0 = start & ~(uintptr_t)15;
+	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
+	const uintptr_t dom = a1 - (uintptr_t)sp.nseg * kCrcSegBytes;   // may wrap below a0
+	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
+
+	uint64_t reg = 0;
+	constexpr int kPf = 4;   // 16-byte loads in flight per lane
+	// The span's first and last byte relative to the lane's chunk, clamped
+	// to a range that keeps every per-block test in 32-bit arithmetic
+	// (outside [-64, 1024 + 64] they only mean "before" / "after").
+	typedef __attribute__((address_space(1))) const uint64_t gcu64;   // global, not flat: loads
+	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
+	auto clamp32 = [](intptr_t v) -> int32_t {
+		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kCrcLaneBytes + 64 ? (intptr_t)kCrcLaneBytes + 64 : v));
+	};
+	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
+	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
+	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
+	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
+		ulonglong2 xs[kPf];
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)(w0 + 16 * u);
+			// words wholly before the data are virtual zeros: no-ops on a zero register
+			xs[u] = make_ulonglong2(0, 0);
+			if (o + 16 > z0) {
+				gcu64* g = reinterpret_cast<gcu64*>(cs + w0 + 16 * u);
+				xs[u].x = g[0];
+				xs[u].y = g[1];
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)(w0 + 16 * u);
+			uint64_t lo = xs[u].x, hi = xs[u].y;
+			const int32_t f = f0 - o;   // first data byte index in this word
+			const int32_t l = l0 - o;   // one past last
+			if (f > -8 || l < 16) {   // only the span's edges need masking
+				const int fc = max(min(f, 24), -8);
+				const int lc = max(min(l, 24), -8);
+				lo &= byte_mask(fc, lc);
+				hi &= byte_mask(fc - 8, lc - 8);
+				// init = ~0: invert the span's first 8 bytes
+				lo ^= byte_mask(fc, fc + 8);
+				hi ^= byte_mask(fc - 8, fc);
+			}
+			reg = slice4(reg, (uint32_t)lo, T);
+			reg = slice4(reg, (uint32_t)(lo >> 32), T);
+			reg = slice4(reg, (uint32_t)hi, T);
+			reg = slice4(reg, (uint32_t)(hi >> 32), T);
+		}
+	}
+	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
+	const uint64_t* L = a.tables + 8 * 256;
+#pragma unroll
+	for (int lv = 0; lv < kCrcLevels; ++lv) {
+		const int d = 1 << lv;
+		const uint32_t plo = (uint32_t)__shfl_down((int)(uint32_t)reg, d, 64);
+		const uint32_t phi = (uint32_t)__shfl_down((int)(uint32_t)(reg >> 32), d, 64);
+		const uint64_t right = ((uint64_t)phi << 32) | plo;
+		const uint64_t shifted = mul_nib(reg, L + lv * kCrcNibTabWords);
+		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
+	}
+	if (lane == 0) a.seg_crc[seg] = reg;
+	}
+}
+#endif
 
 __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
 	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -905,6 +987,202 @@ __device__ void dec_ordered_batch(const DecCmd& c, uint32_t n, bool inplace, uin
 	__builtin_amdgcn_wave_barrier();
 }
 
+// ── windows that are not order-free (in-place deltas whose COPYs move):
+// conflict-free groups, applied by the whole block ──
+//
+// The reference replays such a stream strictly in order, one memmove per
+// command (apply.c:253-267).  Two commands commute unless one writes bytes
+// the other reads or writes, so the window is cut into groups: a group is
+// the longest run of consecutive commands none of which conflicts with an
+// earlier command of the run.  A group's bytes are independent and are
+// copied by all four waves at once in 16-byte chunks; a COPY whose own source
+// and destination overlap (a real memmove) is a group of its own, moved by
+// the block in 4 KiB passes in the direction that never reads a byte it has
+// already written.  Block barriers that order global memory separate groups.
+struct DecGroupLds {
+	uint32_t* src;    // [kDecMaxCmds] COPY source (O or R offset); ADD: payload offset in the window
+	uint32_t* dst;    // [kDecMaxCmds]
+	uint32_t* len;    // [kDecMaxCmds]
+	uint32_t* pre;    // [kDecMaxCmds + 1] exclusive prefix of the 16-byte chunks each command copies
+	int16_t* last;    // [kDecMaxCmds] latest earlier command it conflicts with, -1: none
+	uint8_t* flag;    // [kDecMaxCmds] kGf* bits
+	uint16_t* gs;     // [kDecMaxCmds + 1] group starts, then cnt
+	uint32_t* red;    // [8] block scratch
+};
+constexpr uint8_t kGfCopy = 1, kGfReadsOut = 2, kGfWrites = 4, kGfSelf = 8;
+
+__device__ __forceinline__ bool ov32(uint32_t a, uint32_t al, uint32_t b, uint32_t bl) {
+	return al && bl && a < b + bl && b < a + al;
+}
+
+template <typename WP>
+__device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uint64_t pos, bool inplace, uint8_t* O,
+                                   const uint8_t* R, const uint8_t* D, const DecGroupLds& g) {
+	const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+	static_assert(kDecMaxCmds == 2 * kDecBlock, "two commands per thread in the prefix");
+	// 1. headers -> LDS, flags, chunk counts (two consecutive commands per thread)
+	uint32_t f2[2];
+#pragma unroll
+	for (int u = 0; u < 2; ++u) {
+		const uint32_t c = 2 * tid + u;
+		f2[u] = 0;
+		if (c < cnt) {
+			const uint32_t cx = cmds[c];
+			uint32_t h[4];
+			__builtin_memcpy(h, w + cx, 16);
+			const bool copy = (h[0] & 0xFFu) == 1u;
+			const uint32_t src = copy ? hdr_be32(h, 0) : cx + 9u;
+			const uint32_t dst = copy ? hdr_be32(h, 1) : hdr_be32(h, 0);
+			const uint32_t len = copy ? hdr_be32(h, 2) : hdr_be32(h, 1);
+			const bool noop = inplace && copy && src == dst;   // memmove onto itself
+			const bool writes = len != 0 && !noop;
+			const bool reads_out = inplace && copy && writes;
+			const bool self = reads_out && ov32(src, len, dst, len);
+			g.src[c] = src;
+			g.dst[c] = dst;
+			g.len[c] = len;
+			g.flag[c] = (copy ? kGfCopy : 0) | (reads_out ? kGfReadsOut : 0) | (writes ? kGfWrites : 0) |
+			            (self ? kGfSelf : 0);
+			f2[u] = writes && !self ? (len + 15u) >> 4 : 0u;
+		}
+	}
+	{
+		const uint32_t v = f2[0] + f2[1];
+		const uint32_t incl = dec_incl_scan(v);
+		if (lane == 63) g.red[wave] = incl;
+		__syncthreads();
+		uint32_t off = 0;
+		for (uint32_t k = 0; k < wave; ++k) off += g.red[k];
+		g.pre[2 * tid] = off + incl - v;
+		g.pre[2 * tid + 1] = off + incl - v + f2[0];
+		if (tid == kDecBlock - 1) g.pre[kDecMaxCmds] = off + incl;
+	}
+	__syncthreads();
+	// 2. the latest earlier command each one conflicts with (write/write,
+	//    write/read, read/write; only in-place COPYs read the output)
+	for (uint32_t c = tid; c < cnt; c += kDecBlock) {
+		const uint8_t fc = g.flag[c];
+		int32_t L = -1;
+		if (fc & kGfWrites) {
+			const uint32_t sc = g.src[c], dc = g.dst[c], lc = g.len[c];
+			const bool rc = fc & kGfReadsOut;
+			for (int32_t e = (int32_t)c - 1; e >= 0; --e) {
+				const uint8_t fe = g.flag[e];
+				if (!(fe & kGfWrites)) continue;
+				const uint32_t se = g.src[e], de = g.dst[e], le = g.len[e];
+				if (ov32(de, le, dc, lc) || (rc && ov32(de, le, sc, lc)) || ((fe & kGfReadsOut) && ov32(se, le, dc, lc))) {
+					L = e;
+					break;
+				}
+			}
+		}
+		g.last[c] = (int16_t)L;
+	}
+	__syncthreads();
+	// 3. group starts (wave 0): a group ends before the first command that
+	//    conflicts with one of the group's, and around every self-overlapping move
+	if (wave == 0) {
+		uint32_t s = 0, ng = 1;
+		if (lane == 0) g.gs[0] = 0;
+		for (uint32_t c0 = 1; c0 < cnt; c0 += 64) {
+			const uint32_t c = c0 + lane;
+			const bool live = c < cnt;
+			const int32_t lc = live ? (int32_t)g.last[c] : -1;
+			const bool sf = live && ((g.flag[c] & kGfSelf) || (g.flag[c - 1] & kGfSelf));
+			for (;;) {
+				const uint64_t m = __ballot(live && c > s && (lc >= (int32_t)s || sf));
+				if (!m) break;
+				const uint32_t b = c0 + ffs64(m);
+				if (lane == 0) g.gs[ng] = (uint16_t)b;
+				++ng;
+				s = b;
+			}
+		}
+		if (lane == 0) {
+			g.gs[ng] = (uint16_t)cnt;
+			g.red[4] = ng;
+		}
+	}
+	__syncthreads();
+	const uint32_t ng = g.red[4];
+	// 4. the groups, in stream order
+	for (uint32_t k = 0; k < ng; ++k) {
+		const uint32_t s = g.gs[k], e = g.gs[k + 1];
+		if (e == s + 1 && (g.flag[s] & kGfSelf)) {
+			// one in-place COPY onto an overlapping range: memmove by the block
+			const uint32_t len = g.len[s];
+			const uint8_t* sp = O + g.src[s];
+			uint8_t* dp = O + g.dst[s];
+			const bool backward = dp > sp;
+			const uint32_t npass = (len + 16u * kDecBlock - 1) / (16u * kDecBlock);
+			for (uint32_t q = 0; q < npass; ++q) {
+				const uint32_t pass = backward ? npass - 1 - q : q;
+				const uint32_t b = pass * 16u * kDecBlock + 16u * tid;
+				const uint32_t n = b < len ? umin32(len - b, 16u) : 0u;
+				u32x4_u v{0, 0, 0, 0};
+				uint8_t t[16];
+				if (n == 16) {
+					v = *reinterpret_cast<const u32x4_u*>(sp + b);
+				} else {
+					for (uint32_t i = 0; i < n; ++i) t[i] = sp[b + i];
+				}
+				// every thread's loads of this pass land before any store of
+				// it; later passes read only bytes no earlier pass wrote
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				__syncthreads();
+				if (n == 16) {
+					*reinterpret_cast<u32x4_u*>(dp + b) = v;
+				} else {
+					for (uint32_t i = 0; i < n; ++i) dp[b + i] = t[i];
+				}
+			}
+		} else {
+			// independent commands: chunk j of the group -> thread j % 256
+			const uint32_t j0 = g.pre[s], j1 = g.pre[e];
+			constexpr int kQ = 4;   // chunks in flight per thread
+			for (uint32_t jb = j0; jb < j1; jb += kQ * kDecBlock) {
+				uint8_t* da[kQ];
+				const uint8_t* sa[kQ];
+				u32x4_u v[kQ];
+				uint32_t rem[kQ];
+#pragma unroll
+				for (int u = 0; u < kQ; ++u) {
+					const uint32_t j = jb + u * kDecBlock + tid;
+					rem[u] = 0;
+					da[u] = O;
+					sa[u] = O;
+					if (j < j1) {
+						uint32_t lo = s, hi = e;   // the command holding chunk j: pre[lo] <= j < pre[lo + 1]
+						while (hi - lo > 1) {
+							const uint32_t mid = (lo + hi) >> 1;
+							if (g.pre[mid] <= j) lo = mid;
+							else hi = mid;
+						}
+						const uint32_t boff = 16u * (j - g.pre[lo]);
+						rem[u] = g.len[lo] - boff;
+						const uint8_t fl = g.flag[lo];
+						sa[u] = ((fl & kGfCopy) ? ((fl & kGfReadsOut) ? O : R) + g.src[lo] : D + pos + g.src[lo]) + boff;
+						da[u] = O + g.dst[lo] + boff;
+					}
+					v[u] = rem[u] >= 16 ? *reinterpret_cast<const u32x4_u*>(sa[u]) : u32x4_u{0, 0, 0, 0};
+				}
+#pragma unroll
+				for (int u = 0; u < kQ; ++u) {
+					if (rem[u] >= 16) {
+						*reinterpret_cast<u32x4_u*>(da[u]) = v[u];
+					} else if (rem[u]) {   // the command's last, partial chunk
+						const uint32_t nd = rem[u] >> 2;
+						for (uint32_t i = 0; i < nd; ++i)
+							*reinterpret_cast<u32_u*>(da[u] + 4 * i) = *reinterpret_cast<const u32_u*>(sa[u] + 4 * i);
+						for (uint32_t i = 4 * nd; i < rem[u]; ++i) da[u][i] = sa[u][i];
+					}
+				}
+			}
+		}
+		block_sync_global();   // the group's stores land before the next group reads or writes
+	}
+}
+
 __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void decode_kernel(DecodeArgs a) {
 	const uint32_t i = blockIdx.x;
 	if (i >= a.n) return;
@@ -932,6 +1210,22 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		xs.cum = reinterpret_cast<uint32_t*>(base + 128 * 8);
 		xs.row = reinterpret_cast<uint32_t*>(base + 128 * 8 + 64 * 4);
 		xs.len = reinterpret_cast<uint32_t*>(base + 128 * 8 + 64 * 4 + 128 * 4);
+	}
+	// the grouped apply's arrays, after the four waves' flat-copy scratch
+	DecGroupLds grp;
+	{
+		uint8_t* base = reinterpret_cast<uint8_t*>(NX) + kDecWaves * kScratch;
+		grp.src = reinterpret_cast<uint32_t*>(base);
+		grp.dst = grp.src + kDecMaxCmds;
+		grp.len = grp.dst + kDecMaxCmds;
+		grp.pre = grp.len + kDecMaxCmds;                     // kDecMaxCmds + 1 (+3 pad)
+		grp.red = grp.pre + kDecMaxCmds + 4;                 // 8
+		grp.last = reinterpret_cast<int16_t*>(grp.red + 8);  // kDecMaxCmds
+		grp.gs = reinterpret_cast<uint16_t*>(grp.last + kDecMaxCmds);   // kDecMaxCmds + 1 (+1 pad)
+		grp.flag = reinterpret_cast<uint8_t*>(grp.gs + kDecMaxCmds + 2);
+		static_assert(kDecWaves * kScratch + 4 * (4 * kDecMaxCmds + 4 + 8) + 2 * (2 * kDecMaxCmds + 2) + kDecMaxCmds <=
+		                  3 * kDecWin * 2,
+		              "grouped-apply arrays fit NX");
 	}
 
 #ifdef DG_ONEPASS_PROF
@@ -1207,12 +1501,17 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 					dec_flat_batch(c, inplace, O, R, D, xs);
 					DPROF_ADD(DP_C_FLAT, tq1);
 				}
-			} else if (wave == 0) {
-				for (uint32_t b = 0; b < nb; ++b) {
-					DPROF_INC(DP_BATCHES);
-					const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
-					dec_ordered_batch(c, cnt - 64 * b < 64 ? cnt - 64 * b : 64, inplace, O, R, D, xs);
-				}
+			} else {
+#ifdef DG_AB_SWITCHES
+				if (a.dbg & 0x200) {   // A/B (DG_DEBUG_BITS=0x200): the round-2 one-wave replay
+					if (wave == 0)
+						for (uint32_t b = 0; b < nb; ++b) {
+							const DecCmd c = dec_cmd(w, cmds, 64 * b, cnt, pos);
+							dec_ordered_batch(c, cnt - 64 * b < 64 ? cnt - 64 * b : 64, inplace, O, R, D, xs);
+						}
+				} else
+#endif
+				dec_grouped_window(w, cmds, cnt, pos, inplace, O, R, D, grp);
 			}
 		}
 		DPROF_T(tq2);

@@ -103,7 +103,8 @@ void ref_free(void *p) { free(p); }
 /* ── CPU baseline ───────────────────────────────────────────────────────── */
 
 typedef struct {
-	int algo;               /* 1 onepass, 2 correcting; 11 / 12: decode standard / in-place onepass deltas */
+	int algo;               /* 1 onepass, 2 correcting; 11 / 12: decode standard / in-place onepass
+	                           deltas; 13: decode in-place correcting deltas */
 	size_t n_pairs, len, p, q;
 	uint8_t **r, **v;
 	size_t *lens;           /* per pair |R| = |V| */
@@ -151,7 +152,8 @@ static double now(void)
 
 /* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps
  * algo 1 / 2: encode onepass / correcting; 11 / 12: decode (+ both CRC checks)
- * of standard / in-place (localmin) onepass deltas, rate = sum |V| / time;
+ * of standard / in-place (localmin) onepass deltas, 13: of in-place
+ * (localmin) correcting deltas, rate = sum |V| / time;
  * edit_rate >= 0: C2/C3 substitution pairs; edit_rate < 0: C4 transposition
  * pairs (num_blocks = 8 + i mod 57, -edit_rate percent of blocks moved). */
 int main(int argc, char **argv)
@@ -202,8 +204,9 @@ int main(int argc, char **argv)
 		j.dlens = malloc(j.n_pairs * sizeof(size_t));
 		total_in = 0;
 		for (size_t i = 0; i < j.n_pairs; i++) {
-			j.dlens[i] = j.algo == 12
-			    ? ref_encode_pair_inplace(1, j.r[i], j.lens[i], j.v[i], j.lens[i], j.p, j.q, 0, &j.d[i])
+			j.dlens[i] = j.algo >= 12
+			    ? ref_encode_pair_inplace(j.algo == 13 ? 2 : 1, j.r[i], j.lens[i], j.v[i], j.lens[i], j.p, j.q, 0,
+			                              &j.d[i])
 			    : ref_encode_pair(1, j.r[i], j.lens[i], j.v[i], j.lens[i], j.p, j.q,
 			                      DELTA_BUF_CAP, DELTA_MAX_TABLE_SIZE, &j.d[i]);
 			total_in += (double)j.lens[i];   /* decode rate counts |V| reconstructed */

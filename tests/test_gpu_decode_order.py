@@ -96,3 +96,81 @@ def test_inplace_order_small_windows(dg, ctx, orc):
         R, cmds, vsize = _case(dg, rng, kind, n_r=3000, n_cmds=rng.randint(2, 200))
         d, V = _delta(dg, orc, R, cmds, vsize)
         assert dg.decode(R, d, ctx=ctx) == V, (kind, it)
+
+
+def _moves_case(dg, rng, kind, n=24000):
+    """In-place command lists whose COPYs move: block rotations (a chain in
+    which every COPY overwrites the bytes the previous one read), whole-buffer
+    shifts (one COPY onto an overlapping range: a real memmove, forward and
+    backward), and blocks swapped through an ADD (a broken cycle)."""
+    R = rng.randbytes(n)
+    cmds = []
+    if kind == "rotate":
+        bs = rng.choice([16, 100, 1000, 4096])
+        nb = n // bs
+        for b in range(nb - 1):   # V[b] = R[b + 1]: read before it is overwritten
+            cmds.append(dg.PlacedCopy(src=(b + 1) * bs, dst=b * bs, length=bs))
+        cmds.append(dg.PlacedAdd(dst=(nb - 1) * bs, data=R[:bs]))
+        return R, cmds, nb * bs
+    if kind in ("shift_fwd", "shift_back"):
+        k = rng.choice([1, 7, 15, 16, 17, 300, 5000])
+        if kind == "shift_fwd":   # V = R[k:] + tail: dst < src, overlapping
+            cmds.append(dg.PlacedCopy(src=k, dst=0, length=n - k))
+            cmds.append(dg.PlacedAdd(dst=n - k, data=rng.randbytes(k)))
+        else:                     # V = head + R[:-k]: dst > src, overlapping
+            cmds.append(dg.PlacedCopy(src=0, dst=k, length=n - k))
+            cmds.append(dg.PlacedAdd(dst=0, data=rng.randbytes(k)))
+        return R, cmds, n
+    # "mixed": short moving COPYs in a valid order (each reads bytes no earlier
+    # command wrote), some self-overlapping, no-op COPYs and ADDs between them
+    written = bytearray(n)
+    pos = 0
+    while pos < n - 64:
+        ln = rng.randint(1, 600)
+        if pos + ln > n:
+            break
+        r = rng.random()
+        if r < 0.3:
+            cmds.append(dg.PlacedCopy(src=pos, dst=pos, length=ln))
+        elif r < 0.8:
+            for _ in range(20):
+                src = rng.randrange(0, n - ln)
+                if not any(written[src:src + ln]):
+                    cmds.append(dg.PlacedCopy(src=src, dst=pos, length=ln))
+                    break
+        else:
+            cmds.append(dg.PlacedAdd(dst=pos, data=rng.randbytes(ln)))
+        written[pos:pos + ln] = b"\1" * ln
+        pos += ln
+    return R, cmds, n
+
+
+MOVE_KINDS = ["rotate", "shift_fwd", "shift_back", "mixed"]
+
+
+@pytest.mark.parametrize("kind", MOVE_KINDS)
+def test_inplace_moving_copies(dg, ctx, orc, kind):
+    """Windows that are not order-free go through the conflict-free groups
+    (a chain of dependent COPYs, single COPYs onto overlapping ranges, mixed
+    short moves): the device equals the oracle's sequential memmove replay."""
+    rng = random.Random(2000 + MOVE_KINDS.index(kind))
+    for _ in range(6):
+        R, cmds, vsize = _moves_case(dg, rng, kind)
+        d, V = _delta(dg, orc, R, cmds, vsize)
+        assert dg.decode(R, d, ctx=ctx) == V, kind
+
+
+@pytest.mark.parametrize("policy", ["localmin", "constant"])
+def test_inplace_transposition_deltas(dg, ctx, orc, policy):
+    """Real in-place deltas with moving COPYs: correcting deltas of block
+    transpositions (gen_transpositions.py recipe) converted by dg_make_inplace,
+    decoded on the device against V and against the oracle's replay."""
+    for i in range(24):
+        nb = 8 + (i * 7) % 57
+        R, V = orc.synth_transpose(0xC5000000 + i, nb, 65536 // nb, 50)
+        std = orc.encode(2, R, V, p=16, q=1)
+        d = dg.make_inplace(R, std, policy=policy)
+        assert d[4] == 1
+        rc, Vo = orc.decode(R, d)
+        assert rc == 0 and Vo == V
+        assert dg.decode(R, d, ctx=ctx) == V, (i, policy)

@@ -8,6 +8,12 @@
   dg_make_inplace(localmin)) — sampled deltas byte-identical to the
   reference's own `encode --inplace` chain, all of them decoded on the device
   in one plan and checked against V.
+* C4: the whole 4096-pair transposition batch the bench times, encoded by
+  the correcting plan, sampled pairs bit-exact against the oracle and every
+  pair decoded back to V on the device.
+* C5o: 1024 in-place deltas of C4 transposition pairs (moving COPYs, so the
+  replay order matters): sampled deltas equal to the reference's own
+  `encode correcting --inplace` chain, all decoded on the device in one plan.
 * Work-table pool contention: more long-epoch pairs than pool tables (a
   4-table pool at the default --table-size), every pair checked against the
   oracle.
@@ -140,6 +146,108 @@ def test_c5_inplace_full_batch(dg, ctx, orc, torch_cuda):
         assert bool((dlen == L).all())
         assert bool(torch.equal(dec, ver))
     plan.close()
+
+
+def test_c4_full_batch(dg, ctx, orc, torch_cuda):
+    import ctypes as C
+    torch = torch_cuda
+    n, target, seed = 4096, 262144, 0xC4000000
+    pairs = (dg._lib.Pair * n)()
+    rb, vb = C.c_uint64(), C.c_uint64()
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), None, None, None), "layout")
+    ref = torch.empty(rb.value, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(vb.value, dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), ref.data_ptr(),
+                                                     ver.data_ptr(), None), "synth")
+    lay = [(p.r_off, p.r_len, p.v_off, p.v_len) for p in pairs]
+    out, off, st = _encode(dg, ctx, torch, ref, ver, lay, q=1, algo="correcting")
+    assert int((st != 0).sum()) == 0, st.unique().tolist()
+    offs = off.cpu().tolist()
+    assert offs[0] == 0 and all(offs[i] < offs[i + 1] for i in range(n))
+    for i in [0, 1, 56, 57, 1000, 2047, 3001, n - 1]:
+        nb = 8 + (i % 57)
+        R, V = orc.synth_transpose(seed + i, nb, target // nb, 50)
+        got = bytes(out[offs[i]:offs[i + 1]].cpu().numpy())
+        assert got == orc.encode(2, R, V, p=16, q=1), i
+    descs = (dg._lib.DecodeDesc * n)(*[
+        dg._lib.DecodeDesc(lay[i][0], lay[i][1], offs[i], offs[i + 1] - offs[i], lay[i][2],
+                           max(lay[i][1], lay[i][3])) for i in range(n)])
+    dec = torch.zeros(int(vb.value), dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.check(dg.lib.dg_decode_batch_device(ctx.handle, ref.data_ptr(), out.data_ptr(), descs, n, 0,
+                                            dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(), None),
+              "decode batch")
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert dlen.cpu().tolist() == [x[3] for x in lay]
+    for i in range(n):   # the arena's 16-byte padding between pairs is not part of V
+        e = lay[i][2] + lay[i][3]
+        ver[e:(e + 15) // 16 * 16] = 0
+    assert bool(torch.equal(dec, ver))
+    del ref, ver, out, dec
+    torch.cuda.empty_cache()
+
+
+def test_c5o_ordered_full_batch(dg, ctx, orc, torch_cuda):
+    import ctypes as C
+    import oracle as O
+    torch = torch_cuda
+    n, target, seed = 1024, 262144, 0xC4000000
+    pairs = (dg._lib.Pair * n)()
+    rb, vb = C.c_uint64(), C.c_uint64()
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), None, None, None), "layout")
+    ref = torch.empty(rb.value, dtype=torch.uint8, device="cuda")
+    ver = torch.empty(vb.value, dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed, n, target, 50, pairs,
+                                                     C.byref(rb), C.byref(vb), ref.data_ptr(),
+                                                     ver.data_ptr(), None), "synth")
+    lay = [(p.r_off, p.r_len, p.v_off, p.v_len) for p in pairs]
+    out, off, st = _encode(dg, ctx, torch, ref, ver, lay, q=1, algo="correcting")
+    assert int(st.abs().sum()) == 0
+    offs = off.cpu().tolist()
+    std = out[:offs[-1]].cpu().numpy().tobytes()
+    ref_h = ref.cpu().numpy().tobytes()
+    deltas, moving = [], 0
+    for i, (ro, rl, vo, vl) in enumerate(lay):
+        d = dg.make_inplace(ref_h[ro:ro + rl], std[offs[i]:offs[i + 1]], policy="localmin")
+        deltas.append(d)
+        moving += sum(1 for c in dg.decode_delta(d)[0] if isinstance(c, dg.PlacedCopy) and c.src != c.dst)
+    assert moving > 10 * n      # most COPYs move
+    if O.reference_available():              # the reference's own encode --inplace chain
+        refc = O.Reference()
+        for i in range(0, n, 131):
+            nb = 8 + (i % 57)
+            R, V = orc.synth_transpose(seed + i, nb, target // nb, 50)
+            assert deltas[i] == refc.encode_inplace(2, R, V, p=16, q=1, policy=0), i
+    d_offs = [0]
+    for d in deltas:
+        d_offs.append(d_offs[-1] + len(d))
+    d_dev = torch.frombuffer(bytearray(b"".join(deltas)), dtype=torch.uint8).to("cuda")
+    descs = [(ro, rl, d_offs[i], len(deltas[i]), vo, max(rl, vl)) for i, (ro, rl, vo, vl) in enumerate(lay)]
+    plan = dg.DecodePlan(ctx, descs)
+    dec = torch.zeros(int(vb.value), dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    for i in range(n):   # the arena's padding between pairs is not part of V
+        e = lay[i][2] + lay[i][3]
+        ver[e:(e + 15) // 16 * 16] = 0
+    try:
+        for _ in range(2):   # the plan is reusable
+            dec.zero_()
+            torch.cuda.synchronize()
+            plan.run(ref.data_ptr(), d_dev.data_ptr(), dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(),
+                     ctx.stream)
+            torch.cuda.synchronize()
+            assert int(dst.abs().sum()) == 0, dst.unique().tolist()
+            assert dlen.cpu().tolist() == [x[3] for x in lay]
+            assert bool(torch.equal(dec, ver))
+    finally:
+        plan.close()
 
 
 @pytest.mark.parametrize("mode", ["members", "chain"])

@@ -316,6 +316,39 @@ def test_decode_plan_batch_mixed(dg, ctx, orc, torch_cuda):
                 assert bytes(oc[ds[4]:ds[4] + len(V)].numpy()) == V, i
 
 
+def test_decode_plan_rejects_overlapping_arenas(dg, ctx, orc, torch_cuda):
+    """An output arena overlapping the reference (a one-buffer in-place decode)
+    or the delta bytes is refused before anything is written: the
+    kernel writes the output image before it reads R for the source CRC."""
+    torch = torch_cuda
+    R = bytes(range(256)) * 16
+    V = R[:2000] + b"xyz" + R[2000:]
+    d = orc.encode(ONEPASS, R, V, p=16, q=97)
+    buf = torch.zeros(16384, dtype=torch.uint8, device="cuda")
+    buf[:len(R)] = torch.frombuffer(bytearray(R), dtype=torch.uint8).cuda()
+    dl = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+    olen = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    plan = dg.DecodePlan(ctx, [(0, len(R), 0, len(d), 0, len(V))])
+    before = buf.clone()
+    try:
+        for out_ptr in (buf.data_ptr(),            # out == ref
+                        buf.data_ptr() + 2048,     # out starts inside ref
+                        dl.data_ptr()):            # out == delta
+            with pytest.raises(dg.DeltaError) as e:
+                plan.run(buf.data_ptr(), dl.data_ptr(), out_ptr, olen.data_ptr(), st.data_ptr(), ctx.stream)
+            assert e.value.code == 1
+        torch.cuda.synchronize()
+        assert torch.equal(buf, before)
+        # right after R in the same allocation: disjoint, so it decodes
+        plan.run(buf.data_ptr(), dl.data_ptr(), buf.data_ptr() + len(R), olen.data_ptr(), st.data_ptr(),
+                 ctx.stream)
+        torch.cuda.synchronize()
+        assert int(st.item()) == 0 and bytes(buf[len(R):len(R) + len(V)].cpu().numpy()) == V
+    finally:
+        plan.close()
+
+
 def test_encode_inplace_vs_reference_golden(dg, ctx, orc):
     """dg_encode with DG_OPT_INPLACE (device encode + host CRWI conversion)
     reproduces every reference in-place delta (main.c encode --inplace)."""

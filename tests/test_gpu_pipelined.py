@@ -49,8 +49,47 @@ def test_pipelined_correcting_and_default_q(dg, orc):
         assert d == orc.encode(CORRECTING, R, V, p=16, q=DEFAULT_Q), i
 
 
-def test_pipelined_capacity(dg):
+def test_pipelined_capacity(dg, orc):
     pairs = _pairs(3, 8)
     with pytest.raises(dg.DeltaError) as e:
         dg.encode_pipelined(pairs, "onepass", q=97, out_cap=100)
     assert e.value.code == 7
+    # through the C ABI: the chunks that fit are written and marked DG_OK; every
+    # pair of the chunk that overflowed and of later chunks gets
+    # DG_ERR_CAPACITY and offsets equal to the bytes written so far
+    import ctypes as C
+    L = dg._lib
+    ctx = dg.default_context()
+    pairs = [(bytes(range(256)) * 64, bytes(range(255, -1, -1)) * 64) for _ in range(6)]   # 16 KiB each
+    want = [orc.encode(ONEPASS, R, V, p=16, q=97) for R, V in pairs]
+    n = len(pairs)
+    lay = [(i * 16384, 16384, i * 16384, 16384) for i in range(n)]
+    hr = (C.c_uint8 * (n * 16384)).from_buffer_copy(b"".join(R for R, _ in pairs))
+    hv = (C.c_uint8 * (n * 16384)).from_buffer_copy(b"".join(V for _, V in pairs))
+    cap = len(want[0]) + len(want[1]) + 10          # room for the first chunk (2 pairs) only
+    ho = (C.c_uint8 * cap)()
+    pa = (L.Pair * n)(*[L.Pair(*x) for x in lay])
+    offs = (C.c_uint64 * (n + 1))(*([12345] * (n + 1)))
+    st = (C.c_int32 * n)(*([0] * n))
+    o = L.DiffOptions.make(q=97)
+    rc = dg.lib.dg_encode_pipelined(ctx.handle, ONEPASS, C.addressof(hr), C.addressof(hv), pa, n, C.byref(o),
+                                   2 * 32768, C.addressof(ho), cap, offs, st)
+    assert rc == 7
+    written = len(want[0]) + len(want[1])
+    assert list(st) == [0, 0] + [7] * (n - 2)
+    assert list(offs) == [0, len(want[0]), written] + [written] * (n - 2)
+    assert bytes(ho[:written]) == want[0] + want[1]
+
+
+def test_pipelined_limits_invalidate_cached_plans(dg, orc):
+    """Context limits changed between calls with the same layout: each call
+    builds its plans under the current limits (the cached plans key on them)
+    and the output stays the oracle's in every chain mode (periodic data with
+    q = 97 breaks many verified members)."""
+    ctx = dg.Context(0)
+    pairs = [(bytes(range(256)) * 1024, bytes(range(256)) * 1023 + bytes(256)) for _ in range(3)]
+    want = [orc.encode(ONEPASS, R, V, p=16, q=97) for R, V in pairs]
+    for mode in (dg.MEMBERS_OFF, dg.MEMBERS_ON, dg.MEMBERS_OFF):
+        ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, mode)
+        assert dg.encode_pipelined(pairs, "onepass", q=97, pinned=True, ctx=ctx) == want
+    ctx.close()
