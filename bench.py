@@ -66,11 +66,34 @@ CONFIGS = {
             "1024 in-place deltas of C4 transposition pairs per GPU (device correcting encode + "
             "dg_make_inplace localmin: moving COPYs, order-dependent replay), decode + src/dst CRC "
             "verify on device", "decode"),
+    # stated extra lines: edits that move the diagonal, and
+    # onepass on the C4 transposition pairs, each in the automatic chain mode
+    # and with the plain per-pair chain forced
+    "c3s": (8192, 262144, 0.10, 1, 0xC3500000,
+            "8192 x 256 KiB shift pairs per GPU: 10% edits, 2/3 of them insertions or deletions of "
+            "1-8 bytes (half each), 1/3 byte substitutions; onepass, --table-size 1, automatic chain mode",
+            "onepass"),
+    "c3s_chain": (8192, 262144, 0.10, 1, 0xC3500000,
+                  "c3s with the plain per-pair chain forced (DG_LIMIT_ONEPASS_MEMBERS = 2)", "onepass"),
+    "c4o": (4096, 262144, -50, 1, 0xC4000000,
+            "C4's 4096 transposition pairs of ~256 KiB per GPU, onepass, --table-size 1, automatic chain mode",
+            "onepass"),
+    "c4o_chain": (4096, 262144, -50, 1, 0xC4000000,
+                  "c4o with the plain per-pair chain forced (DG_LIMIT_ONEPASS_MEMBERS = 2)", "onepass"),
+}
+# per-config options: shift pairs (percent of edits that are insertions or
+# deletions), the chain mode forced through the context limit, the config
+# whose CPU baseline a forced-mode line shares
+OPTS = {
+    "c3s": {"indel_pct": 67},
+    "c3s_chain": {"indel_pct": 67, "members": 2, "cpu_as": "c3s"},
+    "c4o_chain": {"members": 2, "cpu_as": "c4o"},
 }
 # oracle/_ref/ref_bench modes: encode onepass / correcting; decode standard / in-place deltas
 REF_MODE = {"onepass": 1, "correcting": 2, "decode": 12, "decode_correcting": 13}
 # CPU baseline samples (pairs): ~1-3 s per timed repetition of the reference's src/c
-CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096), "c5o": (128, 1024)}
+CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096), "c5o": (128, 1024),
+              "c3s": (32, 256), "c4o": (64, 512)}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -133,11 +156,13 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def _ref_bench(cfg, pairs, threads, reps=5):
-    npg, L, rate, q, seed, _, algo = cfg
+def _ref_bench(name, pairs, threads, reps=5):
+    npg, L, rate, q, seed, _, algo = CONFIGS[name]
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     mode = REF_MODE["decode_correcting" if algo == "decode" and rate < 0 else algo]
     cmd = [exe, str(mode), str(pairs), str(L), str(rate), str(seed), str(threads), str(q), str(reps)]
+    if OPTS.get(name, {}).get("indel_pct") is not None:
+        cmd.append(str(OPTS[name]["indel_pct"]))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, check=True)
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -147,6 +172,7 @@ def cpu_baseline(name):
     /root/reference by oracle/Makefile) on the host, a bounded sample of the
     same workload: 1 thread and every thread of this process's CPU share,
     median of 5 timed repetitions each."""
+    name = OPTS.get(name, {}).get("cpu_as", name)
     cfg = CONFIGS[name]
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     if not os.path.exists(exe):
@@ -154,8 +180,8 @@ def cpu_baseline(name):
     n1, nall = CPU_SAMPLE[name]
     threads = cpu_share()
     try:
-        one = _ref_bench(cfg, n1, 1)
-        many = _ref_bench(cfg, nall, threads)
+        one = _ref_bench(name, n1, 1)
+        many = _ref_bench(name, nall, threads)
     except Exception as e:  # noqa: BLE001
         print(f"cpu_baseline failed: {e}", file=sys.stderr)
         return None
@@ -165,6 +191,7 @@ def cpu_baseline(name):
             f"(localmin) {enc} deltas; rate = sum |V| / time" if algo == "decode" else
             f"{algo} chain crc x2 + delta_diff + delta_place_commands + delta_encode; "
             "rate = sum(|R|+|V|) / time")
+    work = f"[{name}] " + work
     return {
         "value": round(many["gib_per_s"], 4),
         "unit": "GiB/s",
@@ -190,8 +217,22 @@ class Rank:
             self.dist.barrier()
 
 
-def make_inputs(dg, ctx, torch, cfg, lo, n, stream):
-    npg, L, rate, q, seed_base, desc, algo = cfg
+def make_inputs(dg, ctx, torch, name, lo, n, stream):
+    npg, L, rate, q, seed_base, desc, algo = CONFIGS[name]
+    indel = OPTS.get(name, {}).get("indel_pct")
+    if indel is not None:   # shift pairs (C3s): substitutions, insertions, deletions
+        import ctypes as C
+        n_edits = int(rate * L + 0.5)
+        pairs = (dg._lib.Pair * max(n, 1))()
+        rb, vb = C.c_uint64(), C.c_uint64()
+        ctx.check(dg.lib.dg_synth_shift_pairs_device(ctx.handle, seed_base + lo, n, L, n_edits, indel, pairs,
+                                                     C.byref(rb), C.byref(vb), None, None, None), "layout")
+        ref = torch.empty(max(rb.value, 1), dtype=torch.uint8, device="cuda")
+        ver = torch.empty(max(vb.value, 1), dtype=torch.uint8, device="cuda")
+        ctx.check(dg.lib.dg_synth_shift_pairs_device(ctx.handle, seed_base + lo, n, L, n_edits, indel, pairs,
+                                                     C.byref(rb), C.byref(vb), ref.data_ptr(), ver.data_ptr(),
+                                                     stream.cuda_stream), "synth")
+        return ref, ver, [(x.r_off, x.r_len, x.v_off, x.v_len) for x in pairs[:n]]
     if rate >= 0:   # substitution pairs (C2/C3/C5)
         n_edits = int(rate * L + 0.5)
         ref = torch.empty(max(n, 1) * L, dtype=torch.uint8, device="cuda")
@@ -238,8 +279,15 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     allr = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")
     lo, hi = allr[R.rank]
     n = hi - lo
-    ref, ver, layout = make_inputs(dg, ctx, torch, cfg, lo, n, stream)
-    plan = dg.EncodePlan(ctx, algo, layout, q=q)
+    ref, ver, layout = make_inputs(dg, ctx, torch, name, lo, n, stream)
+    members = OPTS.get(name, {}).get("members")
+    if members is not None:
+        ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, members)
+    try:
+        plan = dg.EncodePlan(ctx, algo, layout, q=q)
+    finally:
+        if members is not None:
+            ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, dg.MEMBERS_AUTO)
     aligned16 = all((r_off | v_off) % 16 == 0 for r_off, _, v_off, _ in layout)
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
@@ -304,7 +352,9 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": ("synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)"
+        "data": ("synthetic (splitmix64 R, seeded substitutions / insertions / deletions, generated on "
+                 "device)" if OPTS.get(name, {}).get("indel_pct") is not None else
+                 "synthetic (splitmix64 pairs + seeded byte substitutions, generated on device)"
                  if rate >= 0 else
                  "synthetic (splitmix64 R, gen_transpositions.py-style block permutation, "
                  "generated on device)"),
@@ -317,6 +367,7 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "pair_bytes": L,
             "edit_rate": rate if rate >= 0 else None,
             "moved_block_pct": -rate if rate < 0 else None,
+            "indel_pct": OPTS.get(name, {}).get("indel_pct"),
             "table_size_floor": q,
             "q": plan.table_size(0),
             "seed_len": 16,
@@ -377,7 +428,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     ranges = shard.balanced_ranges([1] * total, R.world) if R.rank == 0 else None
     lo, hi = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")[R.rank]
     n = hi - lo
-    ref, ver, layout = make_inputs(dg, ctx, torch, cfg, lo, n, stream)
+    ref, ver, layout = make_inputs(dg, ctx, torch, name, lo, n, stream)
     enc_algo = "onepass" if rate >= 0 else "correcting"
     enc = dg.EncodePlan(ctx, enc_algo, layout, q=q)
     d_arena = torch.empty(enc.output_bound, dtype=torch.uint8, device="cuda")
@@ -485,12 +536,17 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     return line
 
 
-def run_config(name, args, R, dg, ctx, shard, stream):
+def run_config(name, args, R, dg, ctx, shard, stream, cpu=True):
     fn = bench_decode if CONFIGS[name][6] == "decode" else bench_encode
     line = fn(name, args, R, dg, ctx, shard, stream)
+    if cpu:
+        add_cpu_baseline(name, line, args, R)
+    return line
+
+
+def add_cpu_baseline(name, line, args, R):
     if R.world == 1 and R.rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(name)
-    return line
 
 
 # ───────────────────────────── launch ───────────────────────────────────────
@@ -557,7 +613,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--also", default="c3,c4,c5,c5o",
+    ap.add_argument("--also", default="c3,c4,c5,c5o,c3s,c3s_chain,c4o,c4o_chain",
                     help="extra configs measured in the same run, reported under 'also' "
                          "('none' to skip)")
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
@@ -589,12 +645,17 @@ def main():
     ctx = dg.Context(local)
     stream = torch.cuda.Stream()
 
-    line = run_config(args.config, args, R, dg, ctx, shard, stream)
+    # Every device measurement first, the headline config last (on a GPU the
+    # other lines have brought to its running clocks: a cold MI355X reads
+    # 5-8 % low over a 20-step region), then the CPU baselines (host only)
     extras = [c for c in args.also.split(",") if c and c != "none" and c != args.config]
+    also = {name: run_config(name, args, R, dg, ctx, shard, stream, cpu=False) for name in extras}
+    line = run_config(args.config, args, R, dg, ctx, shard, stream, cpu=False)
+    add_cpu_baseline(args.config, line, args, R)
+    for name in extras:
+        add_cpu_baseline(name, also[name], args, R)
     if extras:
-        line["also"] = {}
-        for name in extras:
-            line["also"][name] = run_config(name, args, R, dg, ctx, shard, stream)
+        line["also"] = also
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

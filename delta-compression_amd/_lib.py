@@ -165,6 +165,8 @@ def _load() -> C.CDLL:
         "dg_commands_free": (None, [C.POINTER(Commands)]),
         "dg_make_inplace": (C.c_int, [u8p, sz, u8p, sz, C.c_int, C.POINTER(Buffer), C.POINTER(InplaceStats)]),
         "dg_synth_edit_pairs_device": (C.c_int, [vp, vp, vp, u32, u64, u64, u64, vp]),
+        "dg_synth_shift_pairs_device": (C.c_int, [vp, u64, u32, u64, u64, u32, C.POINTER(Pair),
+                                                  C.POINTER(u64), C.POINTER(u64), vp, vp, vp]),
         "dg_synth_transpose_pairs_device": (C.c_int, [vp, u64, u32, u64, u32, C.POINTER(Pair),
                                                       C.POINTER(u64), C.POINTER(u64), vp, vp, vp]),
     }

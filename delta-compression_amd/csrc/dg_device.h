@@ -254,6 +254,8 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);
+hipError_t launch_synth_shift(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, const uint64_t* v_off,
+                              uint32_t n, uint64_t n_edits, uint32_t pct, hipStream_t st);
 hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,
                                   const SynthCopy* cmds, uint32_t n_cmds, hipStream_t st);
 

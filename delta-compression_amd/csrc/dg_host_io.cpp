@@ -602,6 +602,64 @@ int dg_synth_transpose_pairs_device(dg_context_t* ctx, uint64_t seed_base, uint3
 	return DG_OK;
 }
 
+int dg_synth_shift_pairs_device(dg_context_t* ctx, uint64_t seed_base, uint32_t n, uint64_t pair_len,
+                                uint64_t n_edits, uint32_t indel_pct, dg_pair_t* pairs, uint64_t* ref_bytes,
+                                uint64_t* ver_bytes, uint8_t* d_ref, uint8_t* d_ver, void* stream) {
+	if (!ctx || (n && !pairs) || indel_pct > 100 || pair_len >= (1ull << 31)) return DG_ERR_INVALID_ARG;
+	// |V| of every pair (the edit kinds and sizes, as the device kernel and
+	// or_synth_shift draw them), over a few host threads
+	std::vector<uint64_t> vlen(n);
+	{
+		auto run = [&](uint32_t a, uint32_t b) {
+			for (uint32_t i = a; i < b; ++i) {
+				const uint64_t m = std::min<uint64_t>(n_edits, pair_len);
+				int64_t d = 0;
+				if (m) {
+					const uint64_t s = (seed_base + i) ^ 0x2545F4914F6CDD1DULL, S = pair_len / m;
+					for (uint64_t e = 0; e < m; ++e) {
+						const uint64_t lo = e * S, hi = e + 1 == m ? pair_len : (e + 1) * S;
+						const uint64_t h1 = splitmix_at_host(s, 3 * e + 1), h2 = splitmix_at_host(s, 3 * e + 2);
+						const uint64_t pos = lo + h1 % (hi - lo), u = h2 % 100, k = 1 + (h2 >> 32) % 8;
+						if (2 * u < indel_pct) d += (int64_t)k;
+						else if (u < indel_pct) d -= (int64_t)std::min<uint64_t>(k, hi - pos);
+					}
+				}
+				vlen[i] = (uint64_t)((int64_t)pair_len + d);
+			}
+		};
+		unsigned t = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+		t = std::min<unsigned>(t, std::max(1u, n));
+		std::vector<std::thread> th;
+		for (unsigned k = 1; k < t; ++k) th.emplace_back(run, (uint32_t)((uint64_t)n * k / t), (uint32_t)((uint64_t)n * (k + 1) / t));
+		run(0, (uint32_t)(n / t));
+		for (auto& x : th) x.join();
+	}
+	std::vector<dg::SynthSpan> spans(n);
+	std::vector<uint64_t> voff(n);
+	uint64_t rt = 0, vt = 0;
+	for (uint32_t i = 0; i < n; ++i) {
+		pairs[i] = dg_pair_t{rt, pair_len, vt, vlen[i]};
+		spans[i] = dg::SynthSpan{rt, pair_len, seed_base + i};
+		voff[i] = vt;
+		rt += up16(pair_len);
+		vt += up16(vlen[i]);
+	}
+	if (ref_bytes) *ref_bytes = rt;
+	if (ver_bytes) *ver_bytes = vt;
+	if (!d_ref) return DG_OK;
+	if (!d_ver) return DG_ERR_INVALID_ARG;
+	hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)dg_context_stream(ctx);
+	Dev d_spans, d_voff;
+	if (!d_spans.alloc(sizeof(dg::SynthSpan) * std::max<uint32_t>(n, 1)) || !d_voff.alloc(8ull * std::max<uint32_t>(n, 1)))
+		return DG_ERR_NOMEM;
+	if (n && (hipMemcpyAsync(d_spans.p, spans.data(), sizeof(dg::SynthSpan) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+	          hipMemcpyAsync(d_voff.p, voff.data(), 8ull * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+	          dg::launch_synth_shift(d_ref, d_ver, d_spans.as<dg::SynthSpan>(), d_voff.as<uint64_t>(), n, n_edits,
+	                                 indel_pct, st) != hipSuccess))
+		return DG_ERR_HIP;
+	return hipStreamSynchronize(st) == hipSuccess ? DG_OK : DG_ERR_HIP;
+}
+
 }  // extern "C"
 
 // ───────────────────────────── decode ─────────────────────────────────────

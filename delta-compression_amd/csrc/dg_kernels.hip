@@ -572,11 +572,88 @@ __global__ __launch_bounds__(256) void synth_copy_kernel(uint8_t* ver, const uin
 	for (uint64_t b = threadIdx.x; b < c.len; b += 256) ver[c.dst + b] = ref[c.src + b];
 }
 
+// Shift pairs (oracle/delta_oracle.c or_synth_shift): V = R with one edit per
+// stratum of R — a substitution, or an insertion / deletion of 1..8 bytes.
+// One block per pair; thread t takes a contiguous range of strata, the
+// block's exclusive scan of their length changes places them in V.
+struct ShiftEdit {
+	uint64_t pos, k, bytes;
+	uint32_t kind;   // 0 substitution, 1 insertion, 2 deletion
+};
+__device__ __forceinline__ ShiftEdit shift_edit(uint64_t s, uint64_t e, uint64_t a, uint64_t b, uint32_t pct) {
+	const uint64_t h1 = splitmix_at(s, 3 * e + 1), h2 = splitmix_at(s, 3 * e + 2), h3 = splitmix_at(s, 3 * e + 3);
+	ShiftEdit x;
+	x.pos = a + h1 % (b - a);
+	const uint64_t u = h2 % 100;
+	x.k = 1 + (h2 >> 32) % 8;
+	x.bytes = h3;
+	x.kind = 2 * u < pct ? 1u : (u < pct ? 2u : 0u);
+	if (x.kind == 2 && x.k > b - x.pos) x.k = b - x.pos;
+	return x;
+}
+__global__ __launch_bounds__(256) void synth_shift_kernel(uint8_t* ver, const uint8_t* ref, const SynthSpan* spans,
+                                                          const uint64_t* v_off, uint32_t n_pairs, uint64_t n_edits,
+                                                          uint32_t pct) {
+	__shared__ int64_t part[256];
+	const uint32_t i = blockIdx.x, tid = threadIdx.x;
+	if (i >= n_pairs) return;
+	const SynthSpan sp = spans[i];
+	const uint64_t len = sp.len;
+	const uint8_t* R = ref + sp.off;
+	uint8_t* V = ver + v_off[i];
+	const uint64_t n = n_edits < len ? n_edits : len;
+	if (n == 0) {
+		for (uint64_t b = tid; b < len; b += 256) V[b] = R[b];
+		return;
+	}
+	const uint64_t s = sp.seed ^ 0x2545F4914F6CDD1DULL, S = len / n;
+	const uint64_t e0 = n * tid / 256, e1 = n * (tid + 1) / 256;
+	auto bounds = [&](uint64_t e, uint64_t& a, uint64_t& b) {
+		a = e * S;
+		b = e + 1 == n ? len : (e + 1) * S;
+	};
+	int64_t d = 0;
+	for (uint64_t e = e0; e < e1; ++e) {
+		uint64_t a, b;
+		bounds(e, a, b);
+		const ShiftEdit x = shift_edit(s, e, a, b, pct);
+		d += x.kind == 1 ? (int64_t)x.k : (x.kind == 2 ? -(int64_t)x.k : 0);
+	}
+	part[tid] = d;
+	__syncthreads();
+	int64_t before = 0;
+	for (uint32_t t = 0; t < tid; ++t) before += part[t];
+	uint64_t o = (uint64_t)((int64_t)(e0 * S) + before);
+	for (uint64_t e = e0; e < e1; ++e) {
+		uint64_t a, b;
+		bounds(e, a, b);
+		const ShiftEdit x = shift_edit(s, e, a, b, pct);
+		for (uint64_t p = a; p < x.pos; ++p) V[o++] = R[p];
+		if (x.kind == 1) {
+			for (uint64_t j = 0; j < x.k; ++j) V[o++] = (uint8_t)(x.bytes >> (8 * j));
+			for (uint64_t p = x.pos; p < b; ++p) V[o++] = R[p];
+		} else if (x.kind == 2) {
+			for (uint64_t p = x.pos + x.k; p < b; ++p) V[o++] = R[p];
+		} else {
+			V[o++] = (uint8_t)x.bytes;
+			for (uint64_t p = x.pos + 1; p < b; ++p) V[o++] = R[p];
+		}
+	}
+}
+
 }  // namespace dg
 
 // ───────────────────────────── launchers (C++ linkage, internal) ──────────
 
 namespace dg {
+
+hipError_t launch_synth_shift(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, const uint64_t* v_off,
+                              uint32_t n, uint64_t n_edits, uint32_t pct, hipStream_t st) {
+	if (!n) return hipSuccess;
+	hipLaunchKernelGGL(synth_stream_kernel, dim3(64, n), dim3(256), 0, st, ref, spans, n);
+	hipLaunchKernelGGL(synth_shift_kernel, dim3(n), dim3(256), 0, st, ver, ref, spans, v_off, n, n_edits, pct);
+	return hipGetLastError();
+}
 
 hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* spans, uint32_t n_spans,
                                   const SynthCopy* cmds, uint32_t n_cmds, hipStream_t st) {

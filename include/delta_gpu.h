@@ -435,6 +435,18 @@ int dg_synth_transpose_pairs_device(dg_context_t *ctx, uint64_t seed_base,
                                     uint64_t *ref_bytes, uint64_t *ver_bytes,
                                     uint8_t *d_ref, uint8_t *d_ver,
                                     void *stream);
+/* Shift pairs (a stated extra workload beside C3: edits that move the
+ * diagonal): R_i = the splitmix64 stream of seed seed_base + i, pair_len
+ * bytes; V_i = R_i with n_edits edits, one per equal stratum of R_i,
+ * indel_pct % of them insertions or deletions of 1..8 bytes (half each), the
+ * rest byte substitutions (oracle or_synth_shift).  Layout and the
+ * d_ref == NULL protocol as for dg_synth_transpose_pairs_device. */
+int dg_synth_shift_pairs_device(dg_context_t *ctx, uint64_t seed_base,
+                                uint32_t n_pairs, uint64_t pair_len,
+                                uint64_t n_edits, uint32_t indel_pct,
+                                dg_pair_t *pairs, uint64_t *ref_bytes,
+                                uint64_t *ver_bytes, uint8_t *d_ref,
+                                uint8_t *d_ver, void *stream);
 
 #ifdef __cplusplus
 }

@@ -577,6 +577,48 @@ void or_synth_edits(uint64_t seed, uint8_t *buf, size_t len, uint64_t n_edits)
 	}
 }
 
+#define SHIFT_SALT 0x2545F4914F6CDD1DULL
+
+size_t or_synth_shift(uint64_t seed, size_t len, uint64_t n_edits, uint32_t indel_pct, uint8_t *r,
+                      uint8_t *v)
+{
+	/* Edit e owns stratum [e S, (e + 1) S) of R (the last one runs to the
+	 * end), S = len / n: a position inside it, and a kind (h2 % 100: below
+	 * indel_pct / 2 an insertion, below indel_pct a deletion, else a
+	 * substitution) with k = 1 + (h2 >> 32) % 8 bytes.  Sorted positions by
+	 * construction, so V is the strata in order. */
+	or_synth_random(seed, r, len);
+	uint64_t n = n_edits < len ? n_edits : len;
+	if (n == 0) {
+		memcpy(v, r, len);
+		return len;
+	}
+	uint64_t s = seed ^ SHIFT_SALT, S = len / n;
+	size_t o = 0;
+	for (uint64_t e = 0; e < n; e++) {
+		uint64_t a = e * S, b = e + 1 == n ? len : (e + 1) * S;
+		uint64_t h1 = or_splitmix64_at(s, 3 * e + 1), h2 = or_splitmix64_at(s, 3 * e + 2),
+		         h3 = or_splitmix64_at(s, 3 * e + 3);
+		uint64_t pos = a + h1 % (b - a), u = h2 % 100, k = 1 + (h2 >> 32) % 8;
+		memcpy(v + o, r + a, pos - a);
+		o += pos - a;
+		if (2 * u < indel_pct) {             /* insertion before pos */
+			for (uint64_t i = 0; i < k; i++) v[o++] = (uint8_t)(h3 >> (8 * i));
+			memcpy(v + o, r + pos, b - pos);
+			o += b - pos;
+		} else if (u < indel_pct) {          /* deletion of k bytes at pos */
+			if (k > b - pos) k = b - pos;
+			memcpy(v + o, r + pos + k, b - pos - k);
+			o += b - pos - k;
+		} else {                             /* substitution */
+			v[o++] = (uint8_t)h3;
+			memcpy(v + o, r + pos + 1, b - pos - 1);
+			o += b - pos - 1;
+		}
+	}
+	return o;
+}
+
 #define TRANS_SALT 0x5851F42D4C957F2DULL
 
 size_t or_synth_transpose(uint64_t seed, uint32_t nb, uint32_t mean,

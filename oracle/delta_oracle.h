@@ -97,6 +97,12 @@ void     or_synth_edits(uint64_t seed, uint8_t *buf, size_t len,
 size_t   or_synth_transpose(uint64_t seed, uint32_t num_blocks,
                             uint32_t mean_size, uint32_t perm_pct,
                             uint8_t *r, uint8_t *v, size_t cap);
+/* Shift pairs: R = or_synth_random(seed, len); V = R with n_edits edits,
+ * one per equal stratum of R, indel_pct percent of them insertions or
+ * deletions of 1..8 bytes (half each), the rest byte substitutions (see
+ * DESIGN.md "Synthetic inputs").  Returns |V| (v must hold len + 8 n_edits). */
+size_t   or_synth_shift(uint64_t seed, size_t len, uint64_t n_edits,
+                        uint32_t indel_pct, uint8_t *r, uint8_t *v);
 
 void or_free(void *p);
 

@@ -76,6 +76,8 @@ class Oracle:
         L.or_synth_edits.argtypes = [u64, u8p, sz, u64]
         L.or_synth_transpose.restype = sz
         L.or_synth_transpose.argtypes = [u64, C.c_uint32, C.c_uint32, C.c_uint32, u8p, u8p, sz]
+        L.or_synth_shift.restype = sz
+        L.or_synth_shift.argtypes = [u64, sz, u64, C.c_uint32, u8p, u8p]
         L.or_splitmix64_at.restype = u64
         L.or_splitmix64_at.argtypes = [u64, u64]
         L.or_free.argtypes = [C.c_void_p]
@@ -168,6 +170,13 @@ class Oracle:
         v = (C.c_uint8 * cap)()
         n = self.L.or_synth_transpose(seed, num_blocks, mean, pct, r, v, cap)
         return bytes(r)[:n], bytes(v)[:n]
+
+    def synth_shift(self, seed: int, n: int, n_edits: int, indel_pct: int):
+        """Shift pair (substitutions, insertions and deletions; or_synth_shift)."""
+        r = (C.c_uint8 * max(n, 1))()
+        v = (C.c_uint8 * max(n + 8 * n_edits, 1))()
+        m = self.L.or_synth_shift(seed, n, n_edits, indel_pct, r, v)
+        return bytes(r)[:n], bytes(v)[:m]
 
     def splitmix64_at(self, seed: int, k: int) -> int:
         return self.L.or_splitmix64_at(seed, k)

@@ -107,7 +107,8 @@ typedef struct {
 	                           deltas; 13: decode in-place correcting deltas */
 	size_t n_pairs, len, p, q;
 	uint8_t **r, **v;
-	size_t *lens;           /* per pair |R| = |V| */
+	size_t *lens;           /* per pair |R| (= |V| unless vlens) */
+	size_t *vlens;          /* shift pairs: per pair |V| */
 	uint8_t **d;            /* decode modes: the deltas */
 	size_t *dlens;
 	size_t next;
@@ -131,7 +132,7 @@ static void *worker(void *arg)
 				abort();
 			ob += ol;
 		} else {
-			ob += ref_encode_pair(j->algo, j->r[i], j->lens[i], j->v[i], j->lens[i],
+			ob += ref_encode_pair(j->algo, j->r[i], j->lens[i], j->v[i], j->vlens ? j->vlens[i] : j->lens[i],
 			                      j->p, j->q, DELTA_BUF_CAP,
 			                      DELTA_MAX_TABLE_SIZE, &d);
 		}
@@ -150,12 +151,13 @@ static double now(void)
 	return t.tv_sec + t.tv_nsec / 1e9;
 }
 
-/* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps
+/* usage: ref_bench algo n_pairs pair_len edit_rate seed_base threads q reps [indel_pct]
  * algo 1 / 2: encode onepass / correcting; 11 / 12: decode (+ both CRC checks)
  * of standard / in-place (localmin) onepass deltas, 13: of in-place
  * (localmin) correcting deltas, rate = sum |V| / time;
  * edit_rate >= 0: C2/C3 substitution pairs; edit_rate < 0: C4 transposition
- * pairs (num_blocks = 8 + i mod 57, -edit_rate percent of blocks moved). */
+ * pairs (num_blocks = 8 + i mod 57, -edit_rate percent of blocks moved);
+ * indel_pct given: shift pairs (or_synth_shift, encode modes only). */
 int main(int argc, char **argv)
 {
 	if (argc < 9) {
@@ -172,6 +174,7 @@ int main(int argc, char **argv)
 	int threads = atoi(argv[6]);
 	j.q = strtoull(argv[7], NULL, 0);
 	int reps = atoi(argv[8]);
+	int indel_pct = argc > 9 ? atoi(argv[9]) : -1;   /* >= 0: shift pairs (or_synth_shift) */
 	j.p = DELTA_SEED_LEN;
 	j.r = malloc(j.n_pairs * sizeof(uint8_t *));
 	j.v = malloc(j.n_pairs * sizeof(uint8_t *));
@@ -179,7 +182,14 @@ int main(int argc, char **argv)
 	unsigned long long n_edits = rate > 0 ? (unsigned long long)(rate * (double)j.len + 0.5) : 0;
 	double total_in = 0;
 	for (size_t i = 0; i < j.n_pairs; i++) {
-		if (rate < 0) {
+		if (indel_pct >= 0) {
+			j.r[i] = malloc(j.len);
+			j.v[i] = malloc(j.len + 8 * n_edits + 1);
+			size_t vl = or_synth_shift(seed + i, j.len, n_edits, (uint32_t)indel_pct, j.r[i], j.v[i]);
+			j.lens[i] = j.len;
+			if (!j.vlens) j.vlens = calloc(j.n_pairs, sizeof(size_t));
+			j.vlens[i] = vl;
+		} else if (rate < 0) {
 			uint32_t nb = 8 + (uint32_t)(i % 57), mean = (uint32_t)(j.len / nb);
 			size_t cap = (size_t)nb * (mean * 3 / 2 + 1);
 			j.r[i] = malloc(cap);
@@ -193,7 +203,7 @@ int main(int argc, char **argv)
 			memcpy(j.v[i], j.r[i], j.len);
 			or_synth_edits(seed + i, j.v[i], j.len, n_edits);
 		}
-		total_in += 2.0 * (double)j.lens[i];
+		total_in += (double)j.lens[i] + (double)(j.vlens ? j.vlens[i] : j.lens[i]);
 	}
 	{   /* warm the reference's lazy CRC table before threads start */
 		uint8_t c[8];

@@ -77,6 +77,15 @@ def main():
         out["cases"].append(dict(name=f"c4_onepass_{i}", kind="synth_transpose", seed=0xC4000000 + i,
                                  num_blocks=nb, mean=262144 // nb, pct=50,
                                  **entry(ref, O.ONEPASS, R, V, 16, 1)))
+    for i in range(3):   # shift pairs (C3s): edits that move the diagonal
+        R, V = orc.synth_shift(0xC3500000 + i, 262144, 26214, 67)
+        out["cases"].append(dict(name=f"c3s_{i}", kind="synth_shift", seed=0xC3500000 + i, pair_len=262144,
+                                 n_edits=26214, indel_pct=67, **entry(ref, O.ONEPASS, R, V, 16, 1)))
+    for i, pct in enumerate((5, 100)):   # sparse and indel-only mixes, smaller pairs
+        R, V = orc.synth_shift(0xC3510000 + i, 65536, 300, pct)
+        for algo in (O.ONEPASS, O.CORRECTING):
+            out["cases"].append(dict(name=f"shift_{pct}_{algo}", kind="synth_shift", seed=0xC3510000 + i,
+                                     pair_len=65536, n_edits=300, indel_pct=pct, **entry(ref, algo, R, V, 16, 1)))
     R = orc.synth_random(1, 1 << 20)
     V = orc.synth_random(2, 1 << 20)
     out["cases"].append(dict(name="c1_random_1MiB", kind="synth_random", r_seed=1, v_seed=2,

@@ -155,6 +155,8 @@ def _golden_inputs(orc, case):
         return orc.synth_pair(case["seed"], case["pair_len"], case["n_edits"])
     if kind == "synth_transpose":
         return orc.synth_transpose(case["seed"], case["num_blocks"], case["mean"], case["pct"])
+    if kind == "synth_shift":
+        return orc.synth_shift(case["seed"], case["pair_len"], case["n_edits"], case["indel_pct"])
     return orc.synth_random(case["r_seed"], 1 << 20), orc.synth_random(case["v_seed"], 1 << 20)
 
 

@@ -85,6 +85,8 @@ def test_golden(orc, case):
         R, V = orc.synth_transpose(case["seed"], case["num_blocks"], case["mean"], case["pct"])
     elif kind == "synth_random":
         R, V = orc.synth_random(case["r_seed"], 1 << 20), orc.synth_random(case["v_seed"], 1 << 20)
+    elif kind == "synth_shift":
+        R, V = orc.synth_shift(case["seed"], case["pair_len"], case["n_edits"], case["indel_pct"])
     else:
         raise AssertionError(kind)
     assert _sha(R) == case["r_sha256"] and _sha(V) == case["v_sha256"], "input generator drifted"
