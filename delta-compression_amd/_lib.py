@@ -137,6 +137,7 @@ def _load() -> C.CDLL:
         "dg_encode_plan_table_size": (u64, [vp, u32]),
         "dg_encode_plan_run": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_encode_plan_set_timing": (C.c_int, [vp, C.c_int]),
+        "dg_encode_plan_set_timing_mode": (C.c_int, [vp, C.c_int]),
         "dg_encode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
         "dg_encode_plan_copy_counts_device": (vp, [vp]),
         "dg_encode_plan_destroy": (None, [vp]),
@@ -286,8 +287,10 @@ class EncodePlan:
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)
 
-    def set_timing(self, slots: int = 1):
-        """Record per-stage events for the next runs (ring of `slots` sets)."""
+    def set_timing(self, slots: int = 1, dominant_only: bool = False):
+        """Record per-stage events for the next runs (ring of `slots` sets);
+        dominant_only: only the events around the dominant kernel(s)."""
+        self.ctx.check(lib.dg_encode_plan_set_timing_mode(self.handle, 1 if dominant_only else 0), "timing mode")
         self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(slots)), "set_timing")
 
     def stage_times(self):

@@ -335,11 +335,27 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 // minimum is a ds_min_u32 instead of a memory-side atomic (device-scope
 // atomics are not performed in an XCD's L2), and the finished table — empty
 // slots included — is written out once with coalesced stores (no memset).
+//
+// CRC (a.crc_out != nullptr): the block also computes the CRC-64/XZ of R
+// (delta.h:294-322) from the bytes its lanes already hold, so correcting
+// plans need no separate CRC pass over R.  Iteration k of lane t owns
+// R[32 t + 32 Ki k, +32) (bytes past |R| read as zero); the lane folds its
+// pieces Horner-wise by x^(8 * 32 Ki) (the context's level-5 nibble table),
+// multiplies the result by x^(8 * 32 * (1023 - t)) (the context's per-lane
+// constants, bit-serially, once) and the block XOR-reduces.  That is the
+// raw CRC of R followed by pad = 32 Ki * iterations - |R| zero bytes; the
+// plan's per-pair x^(-8 pad) removes them.  init = ~0 is the first 8 bytes
+// XOR-ed with 0xFF (lane 0, iteration 0), xorout the final inversion.
 constexpr uint32_t kBuildLdsBlock = 1024;
+constexpr uint32_t kCrcPiece = kBuildSeedsPerLane;                    // bytes per lane per iteration
+constexpr uint32_t kCrcStride = kBuildLdsBlock * kBuildSeedsPerLane;  // 32 KiB per iteration
 
+template <bool CRC>
 __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(EncodeArgs a, uint32_t lds_cap) {
 	extern __shared__ uint32_t T[];
 	__shared__ uint64_t nb[256];   // roll61 table
+	__shared__ uint64_t CT[CRC ? 5 * 256 : 1];   // slicing-by-4 tables, then x^(8 * 32 Ki) nibbles
+	__shared__ uint64_t red[CRC ? kBuildLdsBlock / 64 : 1];
 	const uint32_t pair = blockIdx.x;
 	const uint32_t tid = threadIdx.x;
 	const PairPlanDev pp = a.pplan[pair];
@@ -349,11 +365,19 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 	uint32_t* H = a.ctab + pp.tab_base;
 	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) T[i] = kNone;
 	if (tid < 256) nb[tid] = roll_table(tid, a.powc[0]);
+	if constexpr (CRC) {
+		for (uint32_t i = tid; i < 4 * 256; i += kBuildLdsBlock) CT[i] = a.crc_tab[i];
+		if (tid < 256) CT[4 * 256 + tid] = a.crc_tab[8 * 256 + 5 * kCrcNibTabWords + tid];   // level 5: x^(8*32 Ki)
+	}
 	__syncthreads();
 	const uint32_t p = a.p;
-	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
-	if (seeds > 0 && pd.v_len > 0) {
-		const uint8_t* R = a.ref + pd.r_off;
+	const uint64_t rl = pd.r_len;
+	const uint64_t seeds = rl >= p ? rl - p + 1 : 0;
+	const uint8_t* R = a.ref + pd.r_off;
+	const bool build = seeds > 0 && pd.v_len > 0;
+	uint64_t acc = 0;   // CRC: this lane's Horner fold over its pieces
+	const bool crc_wide = CRC && rl >= 64;   // (shorter spans: one thread, byte by byte)
+	if (build || crc_wide) {
 		const uint64_t k = a.kcls[pair];
 		const Ckpt ck = make_ckpt(pp.f_size, pp.f_magic, pp.m, k, pp.q);
 		// the checkpoint path is chosen once per pair (uniform), so the
@@ -374,18 +398,27 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 				}
 				if (pass) __hip_atomic_fetch_min(&T[slot], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 			};
-			for (uint64_t s0 = (uint64_t)tid * kBuildSeedsPerLane; s0 < seeds;
-			     s0 += (uint64_t)kBuildLdsBlock * kBuildSeedsPerLane) {
-				const uint32_t cnt = (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane);
+			// CRC: every lane runs the same number of iterations (the Horner
+			// fold), covering every byte of R; the build only the seeds
+			const uint64_t lim = crc_wide ? rl : (build ? seeds : 0);
+			const uint64_t iters = (lim + kCrcStride - 1) / kCrcStride;
+			for (uint64_t it = 0; it < iters; ++it) {
+				const uint64_t s0 = (uint64_t)tid * kBuildSeedsPerLane + it * kCrcStride;
+				if (!CRC && s0 >= seeds) break;
+				const uint32_t cnt = build && s0 < seeds
+				                         ? (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane)
+				                         : 0u;
+				uint32_t w[12];   // R[s0 .. s0+47), the 48th byte only if it exists
+				bool held = false;
 				if (p == 16 && cnt == kBuildSeedsPerLane) {
-					uint32_t w[12];   // R[s0 .. s0+47), the 48th byte only if it exists
 					__builtin_memcpy(w, R + s0, 32);
-					if (s0 + 48 <= pd.r_len) {
+					if (s0 + 48 <= rl) {
 						__builtin_memcpy(w + 8, R + s0 + 32, 16);
 					} else {
 						__builtin_memcpy(w + 8, R + s0 + 32, 12);
 						w[11] = (uint32_t)R[s0 + 44] | ((uint32_t)R[s0 + 45] << 8) | ((uint32_t)R[s0 + 46] << 16);
 					}
+					held = true;
 					auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
 					// two independent rolling chains (seeds 0..15 and 16..31)
 					uint64_t fa = fp16_dot(w[0], w[1], w[2], w[3]);
@@ -399,7 +432,7 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 						insert(fa, (uint32_t)(s0 + j));
 						insert(fb, (uint32_t)(s0 + 16 + j));
 					}
-				} else {
+				} else if (cnt) {
 					uint64_t fp = window_fp<0>(R + s0, p, a.powc);
 					for (uint32_t j = 0; j < cnt; ++j) {
 						if (j) {
@@ -409,14 +442,54 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 						insert(fp, (uint32_t)(s0 + j));
 					}
 				}
+				if constexpr (CRC) {
+					if (!held) {   // the lane's piece near or past the end of R: byte loads, zeros past |R|
+						for (uint32_t j = 0; j < 8; ++j) w[j] = 0;
+						for (uint32_t j = 0; j < kCrcPiece && s0 + j < rl; ++j) w[j >> 2] |= (uint32_t)R[s0 + j] << (8 * (j & 3));
+					}
+					if (s0 == 0) {   // init = ~0
+						w[0] = ~w[0];
+						w[1] = ~w[1];
+					}
+					uint64_t c = 0;
+#pragma unroll
+					for (uint32_t j = 0; j < 8; ++j) c = slice4(c, w[j], CT);
+					acc = (it ? mul_nib(acc, CT + 4 * 256) : 0ull) ^ c;
+				}
 			}
 		};
 		if (ck.mf.ok && ck.mshift >= 0) run(std::integral_constant<int, 0>{});
 		else if (ck.mf.ok) run(std::integral_constant<int, 1>{});
 		else run(std::integral_constant<int, 2>{});
 	}
+	if constexpr (CRC) {
+		// lane t's fold * x^(8 * 32 * (1023 - t)), XOR over the block
+		uint64_t x = crc_wide ? gf2_mulmod(acc, a.crc_k32[kBuildLdsBlock - 1 - tid]) : 0ull;
+#pragma unroll
+		for (int d = 32; d >= 1; d >>= 1) {
+			const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, d, 64);
+			const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), d, 64);
+			x ^= ((uint64_t)hi << 32) | lo;
+		}
+		if ((tid & 63) == 0) red[tid >> 6] = x;
+	}
 	__syncthreads();
 	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) H[i] = T[i];
+	if constexpr (CRC) {
+		if (tid == 0) {
+			uint64_t crc;
+			if (crc_wide) {
+				uint64_t raw = 0;
+				for (uint32_t w2 = 0; w2 < kBuildLdsBlock / 64; ++w2) raw ^= red[w2];
+				crc = ~gf2_mulmod(raw, pp.crc_unpad);   // drop the zero padding
+			} else {
+				uint64_t c = ~0ull;
+				for (uint64_t i = 0; i < rl; ++i) c = CT[(uint8_t)(c ^ R[i])] ^ (c >> 8);
+				crc = ~c;
+			}
+			a.crc_out[2ull * pair] = crc;
+		}
+	}
 }
 
 // ───────────────────────────── scan ───────────────────────────────────────
@@ -598,13 +671,16 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 // pairs with larger indexes take the memory-atomic build (their tables must
 // have been cleared to ~0 by the caller).  qmin/qmax: index sizes in the batch.
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap,
-                             uint64_t qmin, hipEvent_t ev_built) {
+                             uint64_t qmin, hipEvent_t ev_built, hipEvent_t ev_fork) {
 	(void)p;
 	if (a.n_pairs == 0) return hipSuccess;
 	hipLaunchKernelGGL(correcting_class_kernel, dim3((a.n_pairs + 63) / 64), dim3(64), 0, st, a);
 	if (lds_cap && qmin <= lds_cap) {
 		const size_t tb = 4ull * (a.qmax < lds_cap ? a.qmax : lds_cap);
-		hipLaunchKernelGGL(correcting_build_lds_kernel, dim3(a.n_pairs), dim3(kBuildLdsBlock), tb, st, a, lds_cap);
+		if (a.crc_out)
+			hipLaunchKernelGGL(correcting_build_lds_kernel<true>, dim3(a.n_pairs), dim3(kBuildLdsBlock), tb, st, a, lds_cap);
+		else
+			hipLaunchKernelGGL(correcting_build_lds_kernel<false>, dim3(a.n_pairs), dim3(kBuildLdsBlock), tb, st, a, lds_cap);
 	}
 	if (a.max_seeds && a.qmax > lds_cap) {
 		// 1-D grid, XCD-aware: block b runs on XCD b mod 8, which takes the
@@ -616,8 +692,9 @@ hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, ui
 		hipLaunchKernelGGL(correcting_build_kernel, dim3((uint32_t)blocks), dim3(kBuildBlock), 0, st, a, nchunk, lds_cap);
 	}
 	if (a.stats) hipLaunchKernelGGL(correcting_stats_kernel, dim3(a.n_pairs), dim3(256), 0, st, a);
-	if (ev_built) {
-		const hipError_t e = hipEventRecord(ev_built, st);
+	for (hipEvent_t ev : {ev_built, ev_fork}) {
+		if (!ev) continue;
+		const hipError_t e = hipEventRecord(ev, st);
 		if (e != hipSuccess) return e;
 	}
 	const size_t lds = sizeof(RingEnt) * ((size_t)(a.buf_cap ? a.buf_cap : 1) + 1);

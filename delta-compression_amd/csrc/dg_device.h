@@ -44,6 +44,9 @@ struct PairPlanDev {
 	uint64_t mem_base;         // first member slot (n_chunks x kMemChunkSlots slots)
 	uint32_t chunk_base;       // first chunk (index into the per-chunk member counts)
 	uint32_t n_chunks;         // chunks of kMemChunk positions covering [0, min(|R|,|V|)]
+	// correcting, CRC of R in the build: x^(-8 pad), pad = |R| rounded up to
+	// 32 KiB minus |R| (the build's zero padding)
+	uint64_t crc_unpad;
 };
 
 struct CrcSegDev {        // one wave's CRC segment
@@ -56,7 +59,7 @@ struct CrcSpanDev {
 	uint32_t seg_base;     // first segment index
 	uint32_t nseg;         // number of segments (0 for len < 8)
 	uint32_t which;        // arena selector: 0 = reference arena, 1 = version arena
-	uint32_t pad;
+	uint32_t out;          // index of its CRC in CrcArgs::out
 };
 
 // Precomputed GF(2) constants for the CRC combine steps, as nibble tables:
@@ -119,6 +122,11 @@ struct EncodeArgs {
 	// mismatches, byte mismatches, matches, k, passing seeds whose slot is in
 	// the table (correcting.c:95-98, 137-214, 470-485)
 	uint64_t* stats;
+	// correcting with every R index in LDS: R's CRC-64/XZ computed by the
+	// build (nullptr = a separate CRC pass): out[2 pair] = CRC of R
+	uint64_t* crc_out;
+	const uint64_t* crc_tab;   // the context's CRC tables (CrcArgs::tables)
+	const uint64_t* crc_k32;   // x^(8 * 32 * t), t = 0..1023
 };
 
 constexpr uint32_t kSegTail = 0xFFFFFFFFu;
@@ -242,9 +250,10 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
-// ev_built (nullable): recorded after the R-index build, before the V scan (stage timing)
+// ev_built, ev_fork (nullable): recorded after the R-index build, before the
+// V scan (stage timing; the fork of V's CRC when the build computes R's)
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
-                             hipEvent_t ev_built);
+                             hipEvent_t ev_built, hipEvent_t ev_fork);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after

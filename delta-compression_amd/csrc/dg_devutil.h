@@ -301,4 +301,32 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 	return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
 
+// ── CRC-64/XZ helpers (reflected representation: bit 63 = x^0) ──
+
+// c * K mod P by the constant's nibble tables (tab[16 j + n] = (n x^(4 j)) K)
+__device__ __forceinline__ uint64_t mul_nib(uint64_t c, const uint64_t* __restrict__ tab) {
+	uint64_t r = 0;
+#pragma unroll
+	for (int j = 0; j < 16; ++j) r ^= tab[16 * j + ((c >> (4 * j)) & 15)];
+	return r;
+}
+
+// slicing-by-4 step: the register's low 32 bits absorb one little-endian word
+__device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint64_t* __restrict__ T) {
+	const uint64_t x = crc ^ w;
+	return T[3 * 256 + (x & 0xff)] ^ T[2 * 256 + ((x >> 8) & 0xff)] ^ T[256 + ((x >> 16) & 0xff)] ^
+	       T[(x >> 24) & 0xff] ^ (x >> 32);
+}
+
+// a * b mod P, bit-serial (64 steps; for products by a per-lane constant)
+__device__ __forceinline__ uint64_t gf2_mulmod(uint64_t a, uint64_t b) {
+	uint64_t p = 0;
+#pragma unroll 8
+	for (int i = 0; i < 64; ++i) {
+		p ^= ((a >> (63 - i)) & 1) ? b : 0ull;
+		b = (b >> 1) ^ ((b & 1) ? kCrcPoly : 0ull);
+	}
+	return p;
+}
+
 }  // namespace dg

@@ -106,6 +106,7 @@ struct dg_context {
 	hipStream_t stream = nullptr;
 	uint64_t* d_crc_tables = nullptr;   // slice(8x256) + levels(6x256)
 	uint64_t* d_xinv = nullptr;         // 16
+	uint64_t* d_k32 = nullptr;          // x^(8 * 32 * t), t = 0..1023 (the correcting build's CRC)
 	uint64_t kseg = 0;
 	uint32_t n_cu = 256;                // compute units (grid caps)
 	uint64_t table_pool_bytes = 0;      // DG_LIMIT_TABLE_POOL_BYTES (0 = automatic)
@@ -235,10 +236,18 @@ int dg_context_create(int device, dg_context_t** out) {
 			for (int nb = 0; nb < 16; ++nb)
 				tab[8 * 256 + (kCrcLevels + c) * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
 	}
+	std::vector<uint64_t> k32(1024);
+	{
+		const uint64_t step = gf2_xpow(8ull * 32);
+		k32[0] = 1ULL << 63;
+		for (int t = 1; t < 1024; ++t) k32[t] = gf2_mul(k32[t - 1], step);
+	}
 	if (hipMalloc(&ctx->d_crc_tables, tab.size() * 8) != hipSuccess ||
 	    hipMalloc(&ctx->d_xinv, sizeof xinv) != hipSuccess ||
+	    hipMalloc(&ctx->d_k32, 8 * k32.size()) != hipSuccess ||
 	    hipMemcpy(ctx->d_crc_tables, tab.data(), tab.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-	    hipMemcpy(ctx->d_xinv, xinv, sizeof xinv, hipMemcpyHostToDevice) != hipSuccess) {
+	    hipMemcpy(ctx->d_xinv, xinv, sizeof xinv, hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMemcpy(ctx->d_k32, k32.data(), 8 * k32.size(), hipMemcpyHostToDevice) != hipSuccess) {
 		dg_context_destroy(ctx);
 		return DG_ERR_HIP;
 	}
@@ -252,6 +261,7 @@ void dg_context_destroy(dg_context_t* ctx) {
 	if (ctx->stream) hipStreamSynchronize(ctx->stream);
 	hipFree(ctx->d_crc_tables);
 	hipFree(ctx->d_xinv);
+	hipFree(ctx->d_k32);
 	if (ctx->pin) hipHostFree(ctx->pin);
 	if (ctx->io && ctx->io_free) ctx->io_free(ctx->io);
 	if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -294,8 +304,10 @@ namespace {
 // Segment layout for spans whose device address is 16-byte aligned at
 // offset 0 of the arena (checked at run time): the padded domain is
 // [align_down(off,16), align_up(off+len,16)).
+// outs: where span i's CRC goes in CrcArgs::out (nullptr: at i)
 void plan_crc_spans(const std::vector<dg_span_t>& spans, const std::vector<uint32_t>& which,
-                    std::vector<CrcSpanDev>& sd, std::vector<CrcSegDev>& seg) {
+                    std::vector<CrcSpanDev>& sd, std::vector<CrcSegDev>& seg,
+                    const std::vector<uint32_t>* outs = nullptr) {
 	sd.resize(spans.size());
 	seg.clear();
 	for (size_t i = 0; i < spans.size(); ++i) {
@@ -305,7 +317,7 @@ void plan_crc_spans(const std::vector<dg_span_t>& spans, const std::vector<uint3
 		s.seg_base = (uint32_t)seg.size();
 		s.nseg = 0;
 		s.which = which[i];
-		s.pad = 0;
+		s.out = outs ? (*outs)[i] : (uint32_t)i;
 		if (s.len >= 8) {
 			const uint64_t a0 = s.off & ~15ull, a1 = (s.off + s.len + 15) & ~15ull;
 			s.nseg = (uint32_t)((a1 - a0 + kCrcSegBytes - 1) / kCrcSegBytes);
@@ -366,6 +378,7 @@ struct dg_encode_plan {
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
+	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
@@ -373,6 +386,7 @@ struct dg_encode_plan {
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
 	bool timing = false;
+	int timing_mode = DG_TIMING_ALL;
 	// timing: `slots` sets of kTimingEvents events, one set per run (ring)
 	std::vector<hipEvent_t> ev;
 	uint32_t slots = 0, runs = 0;
@@ -601,18 +615,58 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			c = (uint64_t)((u128)c * kBase % kMersenne);
 		}
 	}
-	// CRC spans: 2 per pair (R then V); arena offsets are rebased at run time
-	std::vector<dg_span_t> spans(2ull * n);
-	std::vector<uint32_t> which(2ull * n);
+	{
+		const char* cb = ab_env("DG_CORR_BUILD");
+		int shm = 0;
+		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
+			shm = 0;
+		// one block's LDS less the 2 KiB roll table, the R CRC's tables
+		// (10 KiB) and reduction words, and some slack
+		const int fixed = 2048 + 10240 + 128 + 256;
+		if (algo == DG_ALGO_CORRECTING && !(cb && strcmp(cb, "global") == 0) && shm > fixed + 4096)
+			P->corr_lds_cap = (uint32_t)((shm - fixed) / 4);
+		// R indexes built in LDS: that build computes R's CRC from the bytes
+		// it holds, and only V's CRC (and R's for the pairs whose index is
+		// built in memory) runs as its own pass, beside the V scan
+		const char* cs = ab_env("DG_CORR_CRC_SEPARATE");
+		P->crc_fused = algo == DG_ALGO_CORRECTING && n && P->corr_lds_cap && P->qmin <= P->corr_lds_cap &&
+		               !(cs && cs[0] == '1');
+	}
+	if (P->crc_fused) {   // x^(-8 pad) of each R's zero padding to a multiple of 32 KiB
+		uint64_t xm8 = 1ULL << 63;
+		for (int b = 0; b < 8; ++b) xm8 = gf2_div_x(xm8);
+		std::map<uint64_t, uint64_t> cache;
+		for (uint32_t i = 0; i < n; ++i) {
+			const uint64_t pad = (32768 - pairs[i].r_len % 32768) % 32768;
+			auto it = cache.find(pad);
+			if (it == cache.end()) {
+				uint64_t r = 1ULL << 63, base = xm8;
+				for (uint64_t e = pad; e; e >>= 1) {
+					if (e & 1) r = gf2_mul(r, base);
+					base = gf2_mul(base, base);
+				}
+				it = cache.emplace(pad, r).first;
+			}
+			P->pp[i].crc_unpad = it->second;
+		}
+	}
+	// CRC spans: 2 per pair (R then V; V only when the build computes R's);
+	// arena offsets are rebased at run time
+	std::vector<dg_span_t> spans;
+	std::vector<uint32_t> which, outs;
 	for (uint32_t i = 0; i < n; ++i) {
-		spans[2ull * i] = dg_span_t{pairs[i].r_off, pairs[i].r_len};
-		spans[2ull * i + 1] = dg_span_t{pairs[i].v_off, pairs[i].v_len};
-		which[2ull * i] = 0;
-		which[2ull * i + 1] = 1;
+		if (!P->crc_fused || P->pp[i].q > P->corr_lds_cap) {
+			spans.push_back(dg_span_t{pairs[i].r_off, pairs[i].r_len});
+			which.push_back(0);
+			outs.push_back(2 * i);
+		}
+		spans.push_back(dg_span_t{pairs[i].v_off, pairs[i].v_len});
+		which.push_back(1);
+		outs.push_back(2 * i + 1);
 	}
 	std::vector<CrcSpanDev> sd;
 	std::vector<CrcSegDev> seg;
-	plan_crc_spans(spans, which, sd, seg);
+	plan_crc_spans(spans, which, sd, seg, &outs);
 	P->n_crc_spans = (uint32_t)sd.size();
 	P->n_crc_segs = (uint32_t)seg.size();
 
@@ -638,7 +692,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_crc_spans_r.alloc(sizeof(CrcSpanDev) * std::max<size_t>(sd.size(), 1));
 	bad |= P->d_crc_segs.alloc(sizeof(CrcSegDev) * std::max<size_t>(seg.size(), 1));
 	bad |= P->d_seg_crc.alloc(8 * std::max<size_t>(seg.size(), 1));
-	bad |= P->d_crc.alloc(8 * std::max<size_t>(sd.size(), 1));
+	bad |= P->d_crc.alloc(16ull * std::max<uint32_t>(n, 1));   // per pair: CRC of R, of V
 	bad |= P->d_tables.alloc(per * P->n_tables);
 	bad |= P->d_locks.alloc(4ull * P->n_tables);
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
@@ -749,15 +803,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->crc_first = cf && cf[0] == '1';
 	const char* sk = ab_env("DG_SKIP_CRC");
 	P->skip_crc = sk && sk[0] == '1';
-	{
-		const char* cb = ab_env("DG_CORR_BUILD");
-		int shm = 0;
-		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
-			shm = 0;
-		// one block's LDS less the 2 KiB byte-out table and some slack
-		if (algo == DG_ALGO_CORRECTING && !(cb && strcmp(cb, "global") == 0) && shm > 4096)
-			P->corr_lds_cap = (uint32_t)((shm - 2048 - 256) / 4);
-	}
+
 	if (!P->serial_crc) {
 		e = hipStreamCreateWithFlags(&P->side, hipStreamNonBlocking);
 		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_fork, hipEventDisableTiming);
@@ -802,6 +848,16 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 }
 
 constexpr int kTimingEvents = 8;
+constexpr uint32_t kTimingAll = 0xFFu;
+// the events a run records: all, or around the dominant kernel(s) only —
+// the member kernel (2, 6), the correcting build and scan (2, 7, 3), the
+// plain onepass kernel (2, 3)
+static uint32_t timing_mask(const dg_encode_plan_t* P) {
+	if (P->timing_mode != DG_TIMING_DOMINANT) return kTimingAll;
+	if (P->members) return (1u << 2) | (1u << 6);
+	if (P->algo == DG_ALGO_CORRECTING) return (1u << 2) | (1u << 7) | (1u << 3);
+	return (1u << 2) | (1u << 3);
+}
 
 int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
@@ -832,23 +888,36 @@ int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** name
 	if (!P || !P->slots || !P->runs) return 0;
 	const uint32_t used = std::min(P->runs, P->slots);
 	const int pairs[8][2] = {{0, 1}, {2, 3}, {3, 4}, {4, 5}, {2, 5}, {2, 6}, {2, 7}, {7, 3}};
-	const int ns = P->algo == DG_ALGO_CORRECTING ? 8 : 6;
+	const uint32_t mask = timing_mask(P);
+	int sel[8], ns = 0;   // the stages whose two events were recorded
+	for (int k = 0; k < 8; ++k) {
+		if (k >= 6 && P->algo != DG_ALGO_CORRECTING) continue;
+		if (k == 5 && P->members == false && mask != kTimingAll) continue;
+		if ((mask >> pairs[k][0] & 1) && (mask >> pairs[k][1] & 1)) sel[ns++] = k;
+	}
+	const int last = (mask >> 5) & 1 ? 5 : (P->members && !(mask >> 3 & 1) ? 6 : 3);
 	double acc[8] = {};
 	for (uint32_t s = 0; s < used; ++s) {
 		hipEvent_t* e = &P->ev[(size_t)kTimingEvents * s];
-		if (hipEventSynchronize(e[5]) != hipSuccess) return 0;
-		for (int k = 0; k < ns; ++k) {
+		if (hipEventSynchronize(e[last]) != hipSuccess) return 0;
+		for (int i = 0; i < ns; ++i) {
 			float t = 0;
-			hipEventElapsedTime(&t, e[pairs[k][0]], e[pairs[k][1]]);
-			acc[k] += t;
+			hipEventElapsedTime(&t, e[pairs[sel[i]][0]], e[pairs[sel[i]][1]]);
+			acc[i] += t;
 		}
 	}
-	int k = 0;
-	for (; k < ns && k < n; ++k) {
-		if (ms) ms[k] = (float)(acc[k] / used);
-		if (names) names[k] = kStageNames[k];
+	int i = 0;
+	for (; i < ns && i < n; ++i) {
+		if (ms) ms[i] = (float)(acc[i] / used);
+		if (names) names[i] = kStageNames[sel[i]];
 	}
-	return k;
+	return i;
+}
+
+int dg_encode_plan_set_timing_mode(dg_encode_plan_t* P, int mode) {
+	if (!P || (mode != DG_TIMING_ALL && mode != DG_TIMING_DOMINANT)) return DG_ERR_INVALID_ARG;
+	P->timing_mode = mode;
+	return DG_OK;
 }
 
 int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t* d_ver,
@@ -870,8 +939,15 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// issue slots they leave idle.
 	hipStream_t cs = P->serial_crc ? st : P->side;
 	if (P->timing) P->cur = &P->ev[(size_t)kTimingEvents * (P->runs++ % P->slots)];
+	// event k on stream s: every stage event, or (DG_TIMING_DOMINANT) only
+	// the ones around the dominant kernel(s) (each extra timing event costs
+	// the run stream a few microseconds)
+	auto rec = [&](int k, hipStream_t s) -> hipError_t {
+		if (!P->timing || !(timing_mask(P) & (1u << k))) return hipSuccess;
+		return hipEventRecord(P->cur[k], s);
+	};
 	auto run_crc = [&]() -> int {
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[0], cs));
+		HIPCHK(ctx, rec(0, cs));
 		CrcArgs a{};
 		a.arena[0] = d_ref;
 		a.arena[1] = d_ver;
@@ -890,13 +966,13 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
 		if (!P->skip_crc)
 			HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[1], cs));
+		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
 	};
 	// differencing -> COPY records + per-pair delta sizes
 	auto run_diff = [&]() -> int {
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[2], st));
-		if (P->timing && !P->members) HIPCHK(ctx, hipEventRecord(P->cur[6], st));
+		HIPCHK(ctx, rec(2, st));
+		if (!P->members) HIPCHK(ctx, rec(6, st));
 		EncodeArgs a{};
 		a.ref = d_ref;
 		a.ver = d_ver;
@@ -938,7 +1014,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				m.csum = P->d_csum.as<uint32_t>();
 				m.cmap = P->d_cmap.as<uint32_t>();
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
-				if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[6], st));
+				HIPCHK(ctx, rec(6, st));
 				a.csum = m.csum;
 				a.cmap = m.cmap;
 				a.seg = P->d_seg.as<uint32_t>();
@@ -956,17 +1032,30 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// the LDS build writes every slot of every index; the global
 			// build only fills, so its tables start empty (~0)
 			if (P->qmax > P->corr_lds_cap) HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
+			if (P->crc_fused) {
+				a.crc_out = P->d_crc.as<uint64_t>();
+				a.crc_tab = ctx->d_crc_tables;
+				a.crc_k32 = ctx->d_k32;
+			}
 			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin,
-			                              P->timing ? P->cur[7] : nullptr));
+			                              P->timing && (timing_mask(P) & (1u << 7)) ? P->cur[7] : nullptr,
+			                              P->crc_fused && !P->serial_crc ? P->ev_fork : nullptr));
 		}
-		if (P->timing && P->algo != DG_ALGO_CORRECTING) HIPCHK(ctx, hipEventRecord(P->cur[7], st));
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[3], st));
+		if (P->algo != DG_ALGO_CORRECTING) HIPCHK(ctx, rec(7, st));
+		HIPCHK(ctx, rec(3, st));
 		return DG_OK;
 	};
 	int rc;
 	if (P->serial_crc) {
 		if ((rc = run_crc()) != DG_OK) return rc;
 		if ((rc = run_diff()) != DG_OK) return rc;
+	} else if (P->crc_fused) {
+		// the build writes R's CRC; V's CRC forks after the build (ev_fork,
+		// recorded by launch_correcting) and runs beside the V scan
+		if ((rc = run_diff()) != DG_OK) return rc;
+		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
+		if ((rc = run_crc()) != DG_OK) return rc;
+		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
 	} else {
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
@@ -983,9 +1072,9 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		// the differencing kernel placed and serialised every delta; only the
 		// header CRCs remain, once the CRC stream has joined
 		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
+		HIPCHK(ctx, rec(4, st));
 		HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
+		HIPCHK(ctx, rec(5, st));
 		return DG_OK;
 	}
 	// 3. exclusive scan of sizes -> packed offsets
@@ -1006,14 +1095,14 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	if (P->ser_block && !P->members) {   // (member mode: records are not gathered)
 		// A/B (DG_SER_BLOCK=1): block-per-pair serialiser, CRCs written in place
 		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
+		HIPCHK(ctx, rec(4, st));
 		HIPCHK(ctx, launch_serialize(s, st));
-		if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
+		HIPCHK(ctx, rec(5, st));
 		return DG_OK;
 	}
 	// 4. serialise everything but the header CRCs (the CRC stream may still
 	//    be running), then join and patch them in
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[4], st));
+	HIPCHK(ctx, rec(4, st));
 	if (P->members) {   // the chains' segment lists, one wave per chunk
 		MemSerArgs m{};
 		m.ver = d_ver;
@@ -1036,7 +1125,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	}
 	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
 	HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
-	if (P->timing) HIPCHK(ctx, hipEventRecord(P->cur[5], st));
+	HIPCHK(ctx, rec(5, st));
 	return DG_OK;
 }
 

@@ -272,12 +272,6 @@ __device__ __forceinline__ uint64_t slice8(uint64_t x, const uint64_t* __restric
 	       T[1 * 256 + ((x >> 48) & 0xff)] ^ T[0 * 256 + (x >> 56)];
 }
 
-__device__ __forceinline__ uint64_t mul_nib(uint64_t c, const uint64_t* __restrict__ tab) {
-	uint64_t r = 0;
-#pragma unroll
-	for (int j = 0; j < 16; ++j) r ^= tab[16 * j + ((c >> (4 * j)) & 15)];
-	return r;
-}
 
 // keep-mask of bytes [lo, hi) within an 8-byte word (0 <= lo, hi <= 8)
 __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
@@ -289,12 +283,6 @@ __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
 	return up & ~dn;
 }
 
-// slicing-by-4 step: the register's low 32 bits absorb one little-endian word
-__device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint64_t* __restrict__ T) {
-	const uint64_t x = crc ^ w;
-	return T[3 * 256 + (x & 0xff)] ^ T[2 * 256 + ((x >> 8) & 0xff)] ^ T[256 + ((x >> 16) & 0xff)] ^
-	       T[(x >> 24) & 0xff] ^ (x >> 32);
-}
 
 // The raw CRC (init 0) of segment j of nseg (64 LB bytes each) of the span
 // [start, start + len) (len >= 8; the span's first 8 bytes inverted: init =
@@ -503,7 +491,7 @@ __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
 		if (t) acc = mul_nib(acc, KS + (1 + t) * kCrcNibTabWords);   // undo the trailing pad bytes (x^-8t)
 		crc = ~acc;
 	}
-	a.out[i] = crc;
+	a.out[sp.out] = crc;
 }
 
 // ───────────────────────────── synthetic inputs ───────────────────────────

@@ -195,8 +195,18 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
  * `n` stage durations (ms), averaged over the last min(runs, slots) runs, and
  * their names ("crc64", "diff", "scan", "serialize+join", "total", "members";
  * "members" is the member kernel alone, inside "diff", 0 in plain chain mode).  Returns
- * the number of stages.  No host synchronisation happens until stage_times. */
+ * the number of stages.  No host synchronisation happens until stage_times.
+ * Correcting plans add "corr_build" and "corr_scan" (the R-index build and
+ * the V scan).  dg_encode_plan_set_timing_mode(plan, DG_TIMING_DOMINANT)
+ * records only the events around the dominant kernel(s) — the member kernel
+ * ("members"), the correcting build and scan ("corr_build", "corr_scan",
+ * "diff") or the onepass kernel ("diff") — and stage_times reports those
+ * only: each timing event costs the run stream a few microseconds, so a
+ * throughput measurement records as few as it needs. */
+#define DG_TIMING_ALL      0
+#define DG_TIMING_DOMINANT 1
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
+int dg_encode_plan_set_timing_mode(dg_encode_plan_t *plan, int mode);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
                                const char **names, int n);
 /* --verbose counters (correcting plans): d_stats = 8 u64 per pair in device

@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=0)
     args = ap.parse_args()
     args.no_cpu_baseline = True
-    args.stage_timing = os.environ.get("AB_TIMING", "all")   # "none": no HIP events in the timed steps
+    # "dominant" (bench.py's default), "all" stage events or "none" in the timed steps
+    args.stage_timing = os.environ.get("AB_TIMING", "dominant")
     import torch
     torch.cuda.set_device(0)
     R = bench.Rank(1, 0, 0, None, torch)

@@ -12,7 +12,7 @@ for r in $(seq $RS); do
  for v in $VS; do
   for c in $CS; do
    DG_LIB_VARIANT=$v timeout -k 10 200 python scripts/ab_bench.py --config $c --steps ${AB_STEPS:-10} --warmup ${AB_WARMUP:-2} > $O/$v.$c.$r.json 2> $O/$v.$c.$r.err || { echo "$v $c rc=$?"; tail -5 $O/$v.$c.$r.err; exit 1; }
-   python3 -c "import json; d=json.loads(open('$O/$v.$c.$r.json').read().strip().splitlines()[-1]); s=d['roofline']['stage_ms']; print('$r $v $c', d['value'], 'ms', d['ms_per_step'], 'diff', s.get('diff'), 'crc', s.get('crc64'))"
+   python3 -c "import json; d=json.loads(open('$O/$v.$c.$r.json').read().strip().splitlines()[-1]); s=d['roofline']['stage_ms']; p=d['roofline'].get('stage_ms_profile',{}); print('$r $v $c', d['value'], 'ms', d['ms_per_step'], 'dom', s, 'crc', p.get('crc64'))"
   done
  done
 done
