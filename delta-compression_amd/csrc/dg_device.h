@@ -117,6 +117,9 @@ struct EncodeArgs {
 	uint32_t* cmap;
 	uint32_t* seg;
 	uint32_t* nseg;            // per pair: segments written
+	// automatic member mode: pairs averaging fewer verified members per chunk
+	// than this run the plain chain (its records as one segment); 0 = never
+	uint32_t route_min;
 	// --verbose diagnostics (correcting; nullptr = off): per pair 8 u64 —
 	// build seeds passing the checkpoint, slots stored, scan checkpoints, fp
 	// mismatches, byte mismatches, matches, k, passing seeds whose slot is in

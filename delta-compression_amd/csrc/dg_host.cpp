@@ -379,6 +379,7 @@ struct dg_encode_plan {
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
+	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
@@ -728,6 +729,12 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		if (fm && fm[0] == '1') want = true;
 		P->members = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
 		             !P->fused && want;
+		// automatic mode: a pair averaging fewer than 2 verified members per
+		// 2 KiB chunk runs the plain chain (C3: ~39; shift and transposition
+		// pairs, whose matches leave diagonal 0: ~0); forced member mode
+		// keeps every pair on the member chain
+		const char* rm = ab_env("DG_ROUTE_MIN");
+		P->route_min = ctx->onepass_members == 0 ? (rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u) : 0u;
 	}
 	if (P->members) {
 		// chunks of kMemChunk positions covering [0, min(|R|, |V|)]; member
@@ -1019,6 +1026,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.cmap = m.cmap;
 				a.seg = P->d_seg.as<uint32_t>();
 				a.nseg = P->d_nseg.as<uint32_t>();
+				a.route_min = P->route_min;
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;

@@ -677,7 +677,7 @@ struct PairResult {
 	int32_t st;
 };
 
-template <bool kMembers, class Src>
+template <bool kMembers, class Src, bool kRouted = false>
 __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
                                              uint32_t* bm) {
@@ -1133,8 +1133,17 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		++nseg;
 		if (lane == 0) a.nseg[pair] = nseg;
 	}
+	constexpr bool routed = kRouted && !members;   // the plain chain for a pair of a member plan
+	if (routed && st == 0 && lane == 0) {
+		// the member serialiser's pieces: every record in one run, then the tail
+		uint4* sg = (uint4*)(a.seg + 4ull * ((uint64_t)pp.chunk_base + 2ull * pair));
+		uint32_t ns = 0;
+		if (nrec) sg[ns++] = make_uint4(0u, nrec, 25u, 0u);
+		sg[ns++] = make_uint4(kSegTail, 0u, (uint32_t)(dsz - 1), v0);
+		a.nseg[pair] = ns;
+	}
 	if (v0 < vl) dsz += 9 + (uint64_t)(vl - v0);   // trailing ADD (:268-275)
-	if (members && (dsz >> 32)) st = 7;   // segment offsets are 32-bit
+	if ((members || routed) && (dsz >> 32)) st = 7;   // segment offsets are 32-bit
 
 	if (tslot >= 0) release_table();
 	if (lane == 0) {
@@ -1159,7 +1168,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 // p = 16, 16-byte aligned pairs: LDS windows (the hot configuration); the
 // member-mode chain is its own instance so the plain chain carries none of
 // its registers
-template <bool kMembers>
+template <bool kMembers, bool kRouted = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
@@ -1168,6 +1177,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
+	if (kMembers || kRouted) {
+		if (a.route_min) {
+			// member plan, automatic mode: a pair whose chunks verified fewer
+			// than route_min members each on average gains nothing from the
+			// members (its matches leave diagonal 0) and runs the plain chain
+			// (the kRouted instance, launched after the member chain's)
+			const uint32_t nch = uni(pp.n_chunks);
+			uint32_t v = 0;
+			for (uint32_t c = lane_id(); c < nch; c += 64) v += a.csum[2ull * (pp.chunk_base + c)];
+			const bool member_pair = rdlane(wave_incl_scan(v), 63) >= a.route_min * nch;
+			if (member_pair != kMembers) return;
+		}
+	}
 	WinSrc src;
 	src.S[0] = a.ver + pd.v_off;
 	src.S[1] = a.ref + pd.r_off;
@@ -1185,7 +1207,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
-	const PairResult res = onepass_pair<kMembers>(src, a, pair, pd, pp, 16u, bm);
+	const PairResult res = onepass_pair<kMembers, WinSrc, kRouted>(src, a, pair, pd, pp, 16u, bm);
 #ifdef DG_REFILL_PROF
 	if (lane_id() == 0) {
 		atomicAdd(&g_refill_prof[0], (unsigned long long)src.refill_cycles);
@@ -1194,7 +1216,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	}
 #endif
 	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
-	if (!kMembers && a.lookback) {
+	if (!kMembers && !kRouted && a.lookback) {
 		// fused placement + serialisation (dg_serialize_wave.h)
 		const uint64_t off = lookback_offset(a.lookback, pair, res.dsz);
 		const uint32_t lane = lane_id();
@@ -1241,11 +1263,14 @@ bool onepass16_selected() { return !force_global_src(); }
 
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
 	if (a.n_pairs == 0) return hipSuccess;
-	if (p == 16 && aligned16 && !force_global_src())
-		if (a.srec)
+	if (p == 16 && aligned16 && !force_global_src()) {
+		if (a.srec) {   // member plan: the member chain, and the plain chain for routed pairs
 			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(a.n_pairs), dim3(64), 0, st, a);
-		else
+			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(a.n_pairs), dim3(64), 0, st, a);
+		} else {
 			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), 0, st, a);
+		}
+	}
 	else if (a.lookback)
 		return hipErrorInvalidValue;   // fused serialisation needs onepass16_kernel
 	else if (p == 16)
