@@ -290,7 +290,9 @@ class EncodePlan:
     def set_timing(self, slots: int = 1, dominant_only: bool = False):
         """Record per-stage events for the next runs (ring of `slots` sets);
         dominant_only: only the events around the dominant kernel(s)."""
-        self.ctx.check(lib.dg_encode_plan_set_timing_mode(self.handle, 1 if dominant_only else 0), "timing mode")
+        mode = getattr(lib, "dg_encode_plan_set_timing_mode", None)   # (older A/B variant builds lack it)
+        if mode is not None:
+            self.ctx.check(mode(self.handle, 1 if dominant_only else 0), "timing mode")
         self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(slots)), "set_timing")
 
     def stage_times(self):
