@@ -304,8 +304,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
                 torch.sub(offs[1:], offs[:-1], out=sizes)
                 gather.global_offsets(gather(R.dist, sizes))
 
-    for _ in range(args.warmup):
-        step()
+    # a checked step first (status, global index), then the W warmup steps
+    # straight into the K timed ones: no host round trip between them, so
+    # the GPU does not idle (and drop its clocks) just before the timer starts
+    step()
     torch.cuda.synchronize()
     bad = int((status != 0).sum().item())
     if bad:
@@ -315,14 +317,16 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         R.dist.all_reduce(tot)
         if int(gather.offsets[-1].item()) != int(tot.item()):
             raise SystemExit(f"{name}: global output index inconsistent")
+    yield None   # prepared: the caller decides when the measurement runs
 
     # In the timed steps only the events around the dominant kernel(s) are
-    # recorded (each timing event costs the run stream microseconds: all of
-    # them took C2 from 0.335 to 0.362 ms per step); the full stage breakdown
-    # comes from an untimed pass of the same steps afterwards.
+    # recorded; the full stage breakdown comes from an untimed pass of the
+    # same steps afterwards.  (The ring keeps the last K runs: the timed ones.)
     timing = getattr(args, "stage_timing", "dominant")
     if timing != "none":
         plan.set_timing(args.steps, dominant_only=timing == "dominant")
+    for _ in range(args.warmup):
+        step()
     elapsed = timed(R, args, step)
     stages = plan.stage_times() if timing != "none" else {}
     plan.set_timing(args.steps)
@@ -421,10 +425,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         # CRC shares the CUs with them)
         line["roofline"]["kernels_ms"] = {"build": round(stages["corr_build"], 4),
                                           "scan": round(stages["corr_scan"], 4)}
+    yield line
     plan.close()
     del ref, ver, out, offs, status, sizes, gather
     torch.cuda.empty_cache()
-    return line
 
 
 def bench_decode(name, args, R, dg, ctx, shard, stream):
@@ -487,16 +491,16 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
         plan.run(ref.data_ptr(), d_dev.data_ptr(), out.data_ptr(), out_len.data_ptr(),
                  status.data_ptr(), stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
     out.zero_()                 # (torch's stream: finished before the decode's stream starts)
     torch.cuda.synchronize()
-    step()
+    step()                      # a checked step, then warmup straight into the timed steps
     torch.cuda.synchronize()
     if int(status.abs().sum()) != 0 or not torch.equal(out[:ver.numel()], ver):
         raise SystemExit(f"{name}: decode failed: status {status.unique().tolist()}")
+    yield None   # prepared
     plan.set_timing(args.steps)
+    for _ in range(args.warmup):
+        step()
     elapsed = timed(R, args, step)
     stages = plan.stage_times()
     elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
@@ -544,15 +548,26 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
                      "path_frac": round(alg / step_s / 1e9 / HBM_PEAK_GBS, 5)},
         "cpu_baseline": None,
     }
+    yield line
     plan.close()
     del ref, ver, out, d_dev, out_len, status
     torch.cuda.empty_cache()
-    return line
+
+
+def prepare_config(name, args, R, dg, ctx, shard, stream):
+    """The config's inputs, plan and a checked step; returns (measure,
+    release): measure() runs the W warmup and K timed steps and returns the
+    line, release() frees the config's device memory."""
+    fn = bench_decode if CONFIGS[name][6] == "decode" else bench_encode
+    g = fn(name, args, R, dg, ctx, shard, stream)
+    next(g)
+    return (lambda: next(g)), (lambda: next(g, None))
 
 
 def run_config(name, args, R, dg, ctx, shard, stream, cpu=True):
-    fn = bench_decode if CONFIGS[name][6] == "decode" else bench_encode
-    line = fn(name, args, R, dg, ctx, shard, stream)
+    measure, release = prepare_config(name, args, R, dg, ctx, shard, stream)
+    line = measure()
+    release()
     if cpu:
         add_cpu_baseline(name, line, args, R)
     return line
@@ -659,12 +674,23 @@ def main():
     ctx = dg.Context(local)
     stream = torch.cuda.Stream()
 
-    # Every device measurement first, the headline config last (on a GPU the
-    # other lines have brought to its running clocks: a cold MI355X reads
-    # 5-8 % low over a 20-step region), then the CPU baselines (host only)
+    # Every device measurement first and the headline config's last, right
+    # after the other lines' (its inputs and plan are prepared up front), on a
+    # GPU that is already at its running clocks: from a cold start the first
+    # 20 steps of C2 read ~12 % slow (0.378 vs 0.331 ms per step over 200).
+    # Then the CPU baselines (host only).
     extras = [c for c in args.also.split(",") if c and c != "none" and c != args.config]
-    also = {name: run_config(name, args, R, dg, ctx, shard, stream, cpu=False) for name in extras}
-    line = run_config(args.config, args, R, dg, ctx, shard, stream, cpu=False)
+    head_measure, head_release = prepare_config(args.config, args, R, dg, ctx, shard, stream)
+    also, release = {}, None
+    for name in extras:
+        if release:
+            release()
+        measure, release = prepare_config(name, args, R, dg, ctx, shard, stream)
+        also[name] = measure()
+    line = head_measure()
+    if release:
+        release()
+    head_release()
     add_cpu_baseline(args.config, line, args, R)
     for name in extras:
         add_cpu_baseline(name, also[name], args, R)
