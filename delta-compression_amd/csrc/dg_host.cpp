@@ -860,10 +860,11 @@ constexpr int kTimingEvents = 8;
 constexpr uint32_t kTimingAll = 0xFFu;
 // the events a run records: all, or around the dominant kernel(s) only —
 // the member kernel (2, 6), the correcting build and scan (2, 7, 3), the
-// plain onepass kernel (2, 3)
+// plain onepass kernel (2, 3); member plans also 3 (the chains after the
+// member kernel: the routed plain chain dominates on data off diagonal 0)
 static uint32_t timing_mask(const dg_encode_plan_t* P) {
 	if (P->timing_mode != DG_TIMING_DOMINANT) return kTimingAll;
-	if (P->members) return (1u << 2) | (1u << 6);
+	if (P->members) return (1u << 2) | (1u << 6) | (1u << 3);   // member kernel, then the chains
 	if (P->algo == DG_ALGO_CORRECTING) return (1u << 2) | (1u << 7) | (1u << 3);
 	return (1u << 2) | (1u << 3);
 }
