@@ -15,6 +15,7 @@ import sys
 
 out_dir, tag, cfg, kre = sys.argv[1:5]
 label = sys.argv[5] if len(sys.argv) > 5 else kre   # the "kernel" field bench.py matches
+name = sys.argv[6] if len(sys.argv) > 6 else cfg    # output name (c4_build: one kernel of c4)
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     per = {}   # kernel name -> values per dispatch; a regex matching several
@@ -39,7 +40,7 @@ res = {
                f"--config {cfg} --also none --steps 5 --warmup 1 --no-cpu-baseline",
 }
 os.makedirs("profiles", exist_ok=True)
-path = f"profiles/{tag}_pmc_traffic_{cfg}.json"
+path = f"profiles/{tag}_pmc_traffic_{name}.json"
 json.dump(res, open(path, "w"), indent=1)
 # keep a copy in gpurun_out so it merges back from the GPU box
 json.dump(res, open(os.path.join(out_dir, os.path.basename(path)), "w"), indent=1)
