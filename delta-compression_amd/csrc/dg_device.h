@@ -263,6 +263,8 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave pe
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0);
+// the CRC with bank-spread tables in 128 KiB of LDS: for a pass that has the GPU to itself
+hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,
                         uint64_t seed_base, uint64_t n_edits, hipStream_t st);

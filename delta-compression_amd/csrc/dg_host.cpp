@@ -379,6 +379,7 @@ struct dg_encode_plan {
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
+	bool crc_wide = false;     // correcting: R's and V's CRC in one wide-table pass before the build
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
@@ -621,17 +622,30 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		int shm = 0;
 		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
 			shm = 0;
-		// one block's LDS less the 2 KiB roll table, the R CRC's tables
+		// Correcting plans compute the CRCs in one of three ways (A/B:
+		// DG_CORR_CRC = wide | fused | beside):
+		//   wide   (default) one pass over R and V before the build, with the
+		//          GPU to itself: bank-spread slicing tables in 128 KiB of LDS
+		//          per CU (crc_segments_wide_kernel), ~2 LDS cycles a lookup;
+		//   fused  the LDS build computes R's CRC from the bytes it holds and
+		//          V's runs beside the V scan;
+		//   beside the onepass arrangement: both CRCs on the side stream
+		//          beside the build (whose 130 KiB-LDS blocks leave it ~1/8 of
+		//          each CU).
+		const char* cm = ab_env("DG_CORR_CRC");
+		int mode = 2;
+		if (cm) mode = !strcmp(cm, "fused") ? 1 : (!strcmp(cm, "beside") ? 0 : 2);
+		if (algo != DG_ALGO_CORRECTING || !n) mode = 0;
+		if (mode == 2 && shm < 8 * 4 * 256 * 16 + 1024) mode = 0;
+		// one block's LDS less the 2 KiB roll table, the fused R CRC's tables
 		// (10 KiB) and reduction words, and some slack
-		const int fixed = 2048 + 10240 + 128 + 256;
+		const int fixed = 2048 + (mode == 1 ? 10240 + 128 : 0) + 256;
 		if (algo == DG_ALGO_CORRECTING && !(cb && strcmp(cb, "global") == 0) && shm > fixed + 4096)
 			P->corr_lds_cap = (uint32_t)((shm - fixed) / 4);
-		// R indexes built in LDS: that build computes R's CRC from the bytes
-		// it holds, and only V's CRC (and R's for the pairs whose index is
-		// built in memory) runs as its own pass, beside the V scan
-		const char* cs = ab_env("DG_CORR_CRC_SEPARATE");
-		P->crc_fused = algo == DG_ALGO_CORRECTING && n && P->corr_lds_cap && P->qmin <= P->corr_lds_cap &&
-		               !(cs && cs[0] == '1');
+		// fused: only R indexes built in LDS compute R's CRC; the others' R
+		// CRCs run in V's pass
+		P->crc_fused = mode == 1 && P->corr_lds_cap && P->qmin <= P->corr_lds_cap;
+		P->crc_wide = mode == 2;
 	}
 	if (P->crc_fused) {   // x^(-8 pad) of each R's zero padding to a multiple of 32 KiB
 		uint64_t xm8 = 1ULL << 63;
@@ -950,7 +964,8 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// forked side stream.  The differencing kernel is enqueued first so its
 	// (long, latency-bound) waves are resident before the CRC waves fill the
 	// issue slots they leave idle.
-	hipStream_t cs = P->serial_crc ? st : P->side;
+	const bool serial = P->serial_crc || P->crc_wide;   // the CRC pass on the run stream, first
+	hipStream_t cs = serial ? st : P->side;
 	if (P->timing) P->cur = &P->ev[(size_t)kTimingEvents * (P->runs++ % P->slots)];
 	// event k on stream s: every stage event, or (DG_TIMING_DOMINANT) only
 	// the ones around the dominant kernel(s) (each extra timing event costs
@@ -977,8 +992,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		// waves (16 per CU), so the CRC neither crowds one round out nor
 		// trails a multi-round batch (C2: 4096 pairs -> 512 blocks)
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
-		if (!P->skip_crc)
-			HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
+		if (!P->skip_crc) {
+			if (P->crc_wide) HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, cs));
+			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
+		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
 	};
@@ -1053,14 +1070,14 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			}
 			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin,
 			                              P->timing && (timing_mask(P) & (1u << 7)) ? P->cur[7] : nullptr,
-			                              P->crc_fused && !P->serial_crc ? P->ev_fork : nullptr));
+			                              P->crc_fused && !serial ? P->ev_fork : nullptr));
 		}
 		if (P->algo != DG_ALGO_CORRECTING) HIPCHK(ctx, rec(7, st));
 		HIPCHK(ctx, rec(3, st));
 		return DG_OK;
 	};
 	int rc;
-	if (P->serial_crc) {
+	if (serial) {
 		if ((rc = run_crc()) != DG_OK) return rc;
 		if ((rc = run_diff()) != DG_OK) return rc;
 	} else if (P->crc_fused) {
@@ -1085,7 +1102,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	if (P->fused) {
 		// the differencing kernel placed and serialised every delta; only the
 		// header CRCs remain, once the CRC stream has joined
-		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
+		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
 		HIPCHK(ctx, rec(4, st));
 		HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
 		HIPCHK(ctx, rec(5, st));
@@ -1108,7 +1125,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	s.n_pairs = P->n;
 	if (P->ser_block && !P->members) {   // (member mode: records are not gathered)
 		// A/B (DG_SER_BLOCK=1): block-per-pair serialiser, CRCs written in place
-		if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
 		HIPCHK(ctx, rec(4, st));
 		HIPCHK(ctx, launch_serialize(s, st));
 		HIPCHK(ctx, rec(5, st));
@@ -1137,7 +1154,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	} else {
 		HIPCHK(ctx, launch_serialize_wave(s, st));
 	}
-	if (!P->serial_crc) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+	if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
 	HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
 	HIPCHK(ctx, rec(5, st));
 	return DG_OK;

@@ -290,11 +290,36 @@ __device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
 // result.  T: the slicing-by-4 tables (LDS); tree: the tree's nibble tables,
 // level l = x^(8 LB 2^l) at tree + 256 l (the context's level tables for
 // 1 KiB lanes; an LDS copy in the decode kernel).
-template <uint32_t LB = kCrcLaneBytes>
+// The slicing tables live in LDS at byte address tb: entry (t, b) at
+// tb + TS t + BS b (TS = 2048, BS = 8 for one plain copy; the bank-spread
+// copies of crc_segments_wide_kernel: TS = 32 Ki, BS = 128, tb + 8 (lane % 16)).
+// 32-bit LDS addresses with the table offsets in the instruction's offset
+// field, and the byte extracts as SDWA shifts: ~3.75 VALU per byte (a
+// generic-pointer version compiled to ~11, 64-bit address arithmetic and
+// if-converted edge masks in every word).
+typedef const __attribute__((address_space(3))) uint64_t lds_cu64;
+__device__ __forceinline__ uint64_t ldsq(uint32_t a) { return *(lds_cu64*)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+	return (uint32_t)(size_t)(lds_cu64*)(const uint64_t*)p;
+}
+// tbh = tb + 2 TS, a second base so every table offset fits the 16-bit
+// offset field of ds_read_b64 (the spread tables span 128 KiB).
+template <uint32_t TS, uint32_t BS>
+__device__ __forceinline__ uint64_t slice4_lds(uint64_t crc, uint32_t w, uint32_t tb, uint32_t tbh) {
+	const uint32_t x = (uint32_t)crc ^ w;
+	return ldsq(tbh + TS + (x & 0xff) * BS) ^ ldsq(tbh + ((x >> 8) & 0xff) * BS) ^
+	       ldsq(tb + TS + ((x >> 16) & 0xff) * BS) ^ ldsq(tb + (x >> 24) * BS) ^ (crc >> 32);
+}
+
+#ifndef DG_CRC_WIDE_PF
+#define DG_CRC_WIDE_PF 4
+#endif
+template <uint32_t LB = kCrcLaneBytes, bool kSpread = false, int kPf = 4>
 __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                 const uint64_t* T, const uint64_t* tree) {
+                                                 uint32_t tb, const uint64_t* tree) {
 	constexpr uint32_t kLaneBytes = LB;
 	constexpr uint64_t kSeg = 64ull * LB;
+	constexpr uint32_t TS = kSpread ? 32768u : 2048u, BS = kSpread ? 128u : 8u;
 	const uint32_t lane = lane_id();
 	const uintptr_t end = start + len;
 	const uintptr_t a0 = start & ~(uintptr_t)15;
@@ -303,11 +328,12 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 	const uintptr_t cs = dom + (uintptr_t)j * kSeg + (uintptr_t)lane * kLaneBytes;
 
 	uint64_t reg = 0;
-	constexpr int kPf = 4;   // 16-byte loads in flight per lane
+	// kPf: 16-byte loads in flight per lane
 	// The span's first and last byte relative to the lane's chunk, clamped
 	// to a range that keeps every per-block test in 32-bit arithmetic
 	// (outside [-64, 1024 + 64] they only mean "before" / "after").
-	typedef __attribute__((address_space(1))) const uint64_t gcu64;   // global, not flat: loads
+	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+	typedef __attribute__((address_space(1))) const v4u gcu128;   // global, not flat: loads
 	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
 	auto clamp32 = [](intptr_t v) -> int32_t {
 		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kLaneBytes + 64 ? (intptr_t)kLaneBytes + 64 : v));
@@ -315,38 +341,37 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
 	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
 	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
+	const uint32_t tbh = __builtin_amdgcn_readfirstlane(0u) + tb + 2 * TS;
 	for (uint32_t w0 = 0; w0 < kLaneBytes; w0 += 16 * kPf) {
-		ulonglong2 xs[kPf];
+		v4u xs[kPf];
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
 			const int32_t o = (int32_t)(w0 + 16 * u);
 			// words wholly before the data are virtual zeros: no-ops on a zero register
-			xs[u] = make_ulonglong2(0, 0);
-			if (o + 16 > z0) {
-				gcu64* g = reinterpret_cast<gcu64*>(cs + w0 + 16 * u);
-				xs[u].x = g[0];
-				xs[u].y = g[1];
-			}
+			xs[u] = v4u{0, 0, 0, 0};
+			if (o + 16 > z0) xs[u] = *reinterpret_cast<gcu128*>(cs + w0 + 16 * u);
 		}
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
 			const int32_t o = (int32_t)(w0 + 16 * u);
-			uint64_t lo = xs[u].x, hi = xs[u].y;
+			v4u x = xs[u];
 			const int32_t f = f0 - o;   // first data byte index in this word
 			const int32_t l = l0 - o;   // one past last
-			if (f > -8 || l < 16) {   // only the span's edges need masking
+			if (__builtin_expect(f > -8 || l < 16, 0)) {   // only the span's edges need masking
 				const int fc = max(min(f, 24), -8);
 				const int lc = max(min(l, 24), -8);
+				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
 				lo &= byte_mask(fc, lc);
 				hi &= byte_mask(fc - 8, lc - 8);
 				// init = ~0: invert the span's first 8 bytes
 				lo ^= byte_mask(fc, fc + 8);
 				hi ^= byte_mask(fc - 8, fc);
+				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 			}
-			reg = slice4(reg, (uint32_t)lo, T);
-			reg = slice4(reg, (uint32_t)(lo >> 32), T);
-			reg = slice4(reg, (uint32_t)hi, T);
-			reg = slice4(reg, (uint32_t)(hi >> 32), T);
+			reg = slice4_lds<TS, BS>(reg, x.x, tb, tbh);
+			reg = slice4_lds<TS, BS>(reg, x.y, tb, tbh);
+			reg = slice4_lds<TS, BS>(reg, x.z, tb, tbh);
+			reg = slice4_lds<TS, BS>(reg, x.w, tb, tbh);
 		}
 	}
 	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
@@ -362,6 +387,30 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 	return uni64(reg);
 }
 
+// The same segments with the slicing tables in 16 copies spread over the LDS
+// banks (128 KiB, one 1024-thread block per CU): entry (t, b) of copy c sits
+// at byte 32 Ki t + 128 b + 8 c, i.e. on bank pair 16 (b & 1) + c, and lane
+// l reads copy l % 16, so of a 32-lane group only lanes l and l + 16 can meet
+// on a bank pair (half the time): ~2 LDS cycles per lookup instead of the
+// ~3.5 of random reads from one copy.  For a CRC pass that has the GPU to
+// itself (correcting plans: before the R-index build).
+constexpr uint32_t kCrcWideBlock = 1024;
+__global__ __launch_bounds__(kCrcWideBlock) void crc_segments_wide_kernel(CrcArgs a) {
+	extern __shared__ uint64_t TW[];   // 4 tables x 256 x 16 copies
+	for (uint32_t i = threadIdx.x; i < 4 * 256 * 16; i += kCrcWideBlock) TW[i] = a.tables[i >> 4];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6;
+	const uint32_t tb = lds_addr(TW) + 8u * (lane_id() & 15u);   // this lane's copy
+	constexpr uint32_t kWaves = kCrcWideBlock / 64;
+	for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_wave<kCrcLaneBytes, true, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg,
+		                                                     sd.j, tb, a.tables + 8 * 256);
+		if (lane_id() == 0) a.seg_crc[seg] = c;
+	}
+}
+
 // segments of seg bytes of a span of len >= 8 bytes at start
 __device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len, uint64_t seg) {
 	const uintptr_t a0 = start & ~(uintptr_t)15, a1 = (start + len + 15) & ~(uintptr_t)15;
@@ -371,7 +420,6 @@ __device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len, uint
 // Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
 // and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
 // tables read through the cache, at most 64 VGPRs.
-#ifndef DG_CRC_R1
 __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	__shared__ uint64_t T[4 * 256];
 	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
@@ -382,92 +430,12 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	     seg += gridDim.x * kCrcWavesPerBlock) {
 		const CrcSegDev sd = a.segs[seg];
 		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_wave((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, T,
+		const uint64_t c = crc_seg_wave((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, lds_addr(T),
 		                                a.tables + 8 * 256);
 		if (lane_id() == 0) a.seg_crc[seg] = c;
 	}
 }
-#else
-__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {   // A/B: the round-1 body (DG_CRC_R1)
-	__shared__ uint64_t T[4 * 256];
-	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6;
-	const uint32_t lane = lane_id();
-	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
-	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
-	     seg += gridDim.x * kCrcWavesPerBlock) {
-	const CrcSegDev sd = a.segs[seg];
-	const CrcSpanDev sp = a.spans[sd.span];
-	const uintptr_t start = (uintptr_t)(a.arena[sp.which] + sp.off);
-	const uintptr_t end = start + sp.len;
-	const uintptr_t a0 = start & ~(uintptr_t)15;
-	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)sp.nseg * kCrcSegBytes;   // may wrap below a0
-	const uintptr_t cs = dom + (uintptr_t)sd.j * kCrcSegBytes + (uintptr_t)lane * kCrcLaneBytes;
 
-	uint64_t reg = 0;
-	constexpr int kPf = 4;   // 16-byte loads in flight per lane
-	// The span's first and last byte relative to the lane's chunk, clamped
-	// to a range that keeps every per-block test in 32-bit arithmetic
-	// (outside [-64, 1024 + 64] they only mean "before" / "after").
-	typedef __attribute__((address_space(1))) const uint64_t gcu64;   // global, not flat: loads
-	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
-	auto clamp32 = [](intptr_t v) -> int32_t {
-		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kCrcLaneBytes + 64 ? (intptr_t)kCrcLaneBytes + 64 : v));
-	};
-	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
-	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
-	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
-	for (uint32_t w0 = 0; w0 < kCrcLaneBytes; w0 += 16 * kPf) {
-		ulonglong2 xs[kPf];
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)(w0 + 16 * u);
-			// words wholly before the data are virtual zeros: no-ops on a zero register
-			xs[u] = make_ulonglong2(0, 0);
-			if (o + 16 > z0) {
-				gcu64* g = reinterpret_cast<gcu64*>(cs + w0 + 16 * u);
-				xs[u].x = g[0];
-				xs[u].y = g[1];
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)(w0 + 16 * u);
-			uint64_t lo = xs[u].x, hi = xs[u].y;
-			const int32_t f = f0 - o;   // first data byte index in this word
-			const int32_t l = l0 - o;   // one past last
-			if (f > -8 || l < 16) {   // only the span's edges need masking
-				const int fc = max(min(f, 24), -8);
-				const int lc = max(min(l, 24), -8);
-				lo &= byte_mask(fc, lc);
-				hi &= byte_mask(fc - 8, lc - 8);
-				// init = ~0: invert the span's first 8 bytes
-				lo ^= byte_mask(fc, fc + 8);
-				hi ^= byte_mask(fc - 8, fc);
-			}
-			reg = slice4(reg, (uint32_t)lo, T);
-			reg = slice4(reg, (uint32_t)(lo >> 32), T);
-			reg = slice4(reg, (uint32_t)hi, T);
-			reg = slice4(reg, (uint32_t)(hi >> 32), T);
-		}
-	}
-	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
-	const uint64_t* L = a.tables + 8 * 256;
-#pragma unroll
-	for (int lv = 0; lv < kCrcLevels; ++lv) {
-		const int d = 1 << lv;
-		const uint32_t plo = (uint32_t)__shfl_down((int)(uint32_t)reg, d, 64);
-		const uint32_t phi = (uint32_t)__shfl_down((int)(uint32_t)(reg >> 32), d, 64);
-		const uint64_t right = ((uint64_t)phi << 32) | plo;
-		const uint64_t shifted = mul_nib(reg, L + lv * kCrcNibTabWords);
-		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
-	}
-	if (lane == 0) a.seg_crc[seg] = reg;
-	}
-}
-#endif
 
 __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
 	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -718,6 +686,16 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 // A grid-stride CRC of 2 blocks per CU leaves the co-running kernel its
 // issue slots instead of queueing 32 CRC waves per CU behind it (C2: step
 // 0.400 -> 0.372 ms).  DG_CRC_BLOCKS overrides (A/B builds only).
+hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
+	if (a.n_segs) {
+		const uint32_t blocks = std::min<uint32_t>(n_cu, (a.n_segs + 15) / 16);
+		hipLaunchKernelGGL(crc_segments_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 4 * 256 * 16, st, a);
+	}
+	if (a.n_spans)
+		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
+	return hipGetLastError();
+}
+
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap) {
 	if (a.n_segs) {
 		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
@@ -1622,7 +1600,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			if (sl[sp] >= 8) {
 				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
-					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, TS, TT);
+					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, lds_addr(TS), TT);
 					acc = (last != ~0u ? mul_nib(acc, TK) : 0ull) ^ c;   // TK: x^(8 * 64 KiB) = 4 segments
 					last = j;
 				}

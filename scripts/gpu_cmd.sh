@@ -1,7 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/default.json 2> gpurun_out/default.err || { echo bench failed; tail -5 gpurun_out/default.err; exit 1; }
-python3 -c "
-import json; d=json.loads(open('gpurun_out/default.json').read().strip().splitlines()[-1])
-for k,v in [('c2',d)]+list(d['also'].items()): print(k, v['value'], v['ms_per_step'], v['roofline']['frac'], v['roofline']['path_frac'], v['roofline']['stage_ms'], (v.get('cpu_baseline') or {}).get('value'))"
+for r in 1 2; do
+for v in ab pf8 pf16; do
+  env DG_LIB_VARIANT=$v timeout -k 10 300 python scripts/ab_bench.py --config c4 --steps 20 --warmup 5 > gpurun_out/c4_ab.json 2> gpurun_out/c4_ab.err || { echo "c4 $v failed"; tail -5 gpurun_out/c4_ab.err; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/c4_ab.json').read().strip().splitlines()[-1]); print('c4 $v', d['value'], d['ms_per_step'], d['roofline']['stage_ms'], d['roofline']['stage_ms_profile'].get('crc64'))"
+done
+done
+bash scripts/pmc_probe.sh gpurun_out/probe8 c4 crc_segments_wide TCP_TOTAL_CACHE_ACCESSES_sum,TCP_TCC_READ_REQ_sum,TCP_PENDING_STALL_CYCLES_sum,GRBM_GUI_ACTIVE
