@@ -71,6 +71,13 @@ constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
 // lanes x^(8 * 256), x^(8 * 512) (its first two tree levels) and x^(8 * 48 KiB)
 constexpr int kCrcFinTabs = 1 + 16 + 3 + 3;
 constexpr int kCrcFinX256 = 20, kCrcFinX512 = 21, kCrcFinX48K = 22;   // indices in F
+// after F: the row-interleaved segment tables (crc_seg_rows): for 16- and
+// 8-byte pieces, U_j = T advanced by (64 PB - 1 - j) bytes (16 and 8 tables
+// of 256), then the per-lane constants x^(-8 PB l), l = 0..63, for PB = 16, 8
+constexpr uint32_t kCrcRowsOff = 8 * 256 + (kCrcLevels + kCrcFinTabs) * kCrcNibTabWords;
+constexpr uint32_t kCrcRows16 = kCrcRowsOff, kCrcRows8 = kCrcRowsOff + 16 * 256;
+constexpr uint32_t kCrcRowK16 = kCrcRowsOff + 24 * 256, kCrcRowK8 = kCrcRowK16 + 64;
+constexpr uint32_t kCrcTabWords = kCrcRowK8 + 64;
 
 
 struct EncodeArgs {
@@ -258,11 +265,12 @@ hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint3
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
                              hipEvent_t ev_built, hipEvent_t ev_fork);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
-hipError_t launch_serialize(const SerArgs& s, hipStream_t st);        // block per pair, writes the CRCs
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0);
+// rows: the row-interleaved pass (16 KiB LDS per block) instead of the
+// lane-contiguous one (8 KiB)
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, bool rows = true);
 // the CRC with bank-spread tables in 128 KiB of LDS: for a pass that has the GPU to itself
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);

@@ -201,7 +201,7 @@ int dg_context_create(int device, dg_context_t** out) {
 
 	// CRC tables: slicing-by-8 and nibble tables of the combine constants
 	// + the finaliser's constants: x^(8 kCrcSegBytes) and the 16 pad inverses
-	std::vector<uint64_t> tab(8 * 256 + (kCrcLevels + kCrcFinTabs) * kCrcNibTabWords);
+	std::vector<uint64_t> tab(kCrcTabWords);
 	for (int i = 0; i < 256; ++i) {
 		uint64_t c = (uint64_t)i;
 		for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
@@ -235,6 +235,29 @@ int dg_context_create(int device, dg_context_t** out) {
 		for (int j = 0; j < 16; ++j)
 			for (int nb = 0; nb < 16; ++nb)
 				tab[8 * 256 + (kCrcLevels + c) * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
+	}
+	{
+		// row-interleaved segment tables: byte j of a PB-byte piece followed by
+		// the 64 PB - PB bytes of the other lanes' pieces of its row
+		std::vector<uint64_t> adv(256);
+		for (int i = 0; i < 256; ++i) adv[i] = tab[i];   // T advanced by 0 bytes
+		for (int n = 1; n <= 1023; ++n) {
+			for (int i = 0; i < 256; ++i) adv[i] = (adv[i] >> 8) ^ tab[adv[i] & 0xff];
+			if (n >= 1008)   // n = 1023 - j
+				for (int i = 0; i < 256; ++i) tab[kCrcRows16 + (1023 - n) * 256 + i] = adv[i];
+			if (n >= 504 && n <= 511)   // n = 511 - j
+				for (int i = 0; i < 256; ++i) tab[kCrcRows8 + (511 - n) * 256 + i] = adv[i];
+		}
+		uint64_t z = 1ULL << 63;   // x^0
+		for (int l = 0; l < 64; ++l) {   // x^(-8*16*l), x^(-8*8*l)
+			tab[kCrcRowK16 + l] = z;
+			for (int b = 0; b < 128; ++b) z = gf2_div_x(z);
+		}
+		z = 1ULL << 63;
+		for (int l = 0; l < 64; ++l) {
+			tab[kCrcRowK8 + l] = z;
+			for (int b = 0; b < 64; ++b) z = gf2_div_x(z);
+		}
 	}
 	std::vector<uint64_t> k32(1024);
 	{
@@ -384,7 +407,6 @@ struct dg_encode_plan {
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
-	bool ser_block = false;    // DG_SER_BLOCK=1: block-per-pair serialiser (A/B)
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
 	bool timing = false;
@@ -816,8 +838,6 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	}
 	const char* sc = ab_env("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
-	const char* sb = ab_env("DG_SER_BLOCK");
-	P->ser_block = sb && sb[0] == '1';
 	const char* db = ab_env("DG_DEBUG_BITS");
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = ab_env("DG_CRC_FIRST");
@@ -906,9 +926,8 @@ int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 
 // Per-run events: 0/1 around the CRC kernels (side stream), 2/3 around the
 // differencing kernel(s), 4 after the scan, 5 after serialisation + the CRC
-// join + the header patch (DG_SER_BLOCK=1 / DG_FUSED=1: the join falls before
-// 4), 6 after the member kernel (member mode; else with 2), 7 after the
-// correcting R-index build (before the V scan; onepass: with 3).  Stages
+// join + the header patch (DG_FUSED=1: the join falls before 4), 6 after
+// the member kernel (member mode; else with 2), 7 after the correcting R-index build (before the V scan; onepass: with 3).  Stages
 // corr_build (2..7) and corr_scan (7..3) are reported for correcting plans only.
 // Returns the mean over the runs recorded since set_timing (at most `slots`).
 int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** names, int n) {
@@ -994,7 +1013,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
 		if (!P->skip_crc) {
 			if (P->crc_wide) HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, cs));
-			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u)));
+			// (member plans keep the 8 KiB-LDS lane-contiguous pass: the row pass's
+			// 16 KiB blocks find no room beside the member kernel and trail it)
+			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
+			                            !P->members));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
@@ -1123,14 +1145,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	s.out_cap = out_cap;
 	s.status = d_status;
 	s.n_pairs = P->n;
-	if (P->ser_block && !P->members) {   // (member mode: records are not gathered)
-		// A/B (DG_SER_BLOCK=1): block-per-pair serialiser, CRCs written in place
-		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
-		HIPCHK(ctx, rec(4, st));
-		HIPCHK(ctx, launch_serialize(s, st));
-		HIPCHK(ctx, rec(5, st));
-		return DG_OK;
-	}
 	// 4. serialise everything but the header CRCs (the CRC stream may still
 	//    be running), then join and patch them in
 	HIPCHK(ctx, rec(4, st));
@@ -1209,7 +1223,7 @@ extern "C" int dg_crc64_xz_batch_device(dg_context_t* ctx, const uint8_t* d_aren
 	a.out = d_crc;
 	a.xinv = ctx->d_xinv;
 	a.kseg = ctx->kseg;
-	HIPCHK(ctx, launch_crc(a, st));
+	HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, st));   // alone on the device: the wide pass
 	HIPCHK(ctx, hipStreamSynchronize(st));   // the temporaries die here
 	return DG_OK;
 }

@@ -5,7 +5,7 @@
 //   onepass_kernel   one wave64 per pair, onepass differencing
 //       (src/c/onepass.c:32-297) in its epoch form
 //   scan_sizes_kernel  exclusive scan of per-pair delta sizes
-//   serialize_kernel   placement + DLT\x03 serialisation
+//   serialize_wave_kernel   placement + DLT\x03 serialisation
 //       (src/c/apply.c:136-164, src/c/encoding.c:39-90)
 //   synth_*            synthetic batch generators (bench/test inputs)
 //
@@ -72,185 +72,6 @@ __device__ __forceinline__ void put_u32be(uint8_t* o, uint32_t x) {
 
 
 
-// One 256-thread block per pair.  Commands are in V order with sequential
-// destinations (apply.c:136-164): every gap between consecutive COPYs is one
-// ADD of V bytes, so the COPY records alone describe the delta.
-//
-// Records are taken 256 at a time (one per thread).  A block scan gives each
-// command's offset; the tile's bytes are assembled in LDS (headers by their
-// thread, ADD payloads copied from V by their thread, or by the whole block
-// when long) and then written out as coalesced dwords.  A tile whose bytes do
-// not fit the staging buffer is written directly instead.
-constexpr uint32_t kSerStage = 20480;
-
-__device__ __forceinline__ void put_u32be_lds(uint8_t* o, uint32_t x) {
-	o[0] = (uint8_t)(x >> 24);
-	o[1] = (uint8_t)(x >> 16);
-	o[2] = (uint8_t)(x >> 8);
-	o[3] = (uint8_t)x;
-}
-
-__global__ __launch_bounds__(256) void serialize_kernel(SerArgs s) {
-	const uint32_t pair = blockIdx.x;
-	const uint32_t tid = threadIdx.x;
-	__shared__ uint64_t scan[256];
-	__shared__ uint32_t big_dst[256], big_src[256], big_len[256];
-	__shared__ uint32_t n_big;
-	__shared__ uint64_t pos_sh;
-	__shared__ __attribute__((aligned(16))) uint8_t stage[kSerStage + 8];
-
-	const uint64_t base = s.offsets[pair];
-	const uint64_t end = s.offsets[pair + 1];
-	if (end > s.out_cap) {
-		if (tid == 0) s.status[pair] = 7;
-		return;
-	}
-	if (s.status[pair] != 0) return;
-	const PairDev pd = s.pairs[pair];
-	const PairPlanDev pp = s.pplan[pair];
-	const uint8_t* V = s.ver + pd.v_off;
-	const uint64_t vl = pd.v_len;
-	const uint32_t n = s.n_rec[pair];
-	const uint32_t W = s.rec_words;
-	const uint32_t* rec = s.rec + (uint64_t)W * pp.rec_base;
-	uint8_t* out = s.out + base;
-
-	if (tid == 0) {
-		out[0] = 'D'; out[1] = 'L'; out[2] = 'T'; out[3] = 3;
-		out[4] = 0;                       // standard delta
-		put_u32be(out + 5, (uint32_t)vl);
-		const uint64_t cs = s.crc[2ull * pair], cd = s.crc[2ull * pair + 1];
-		for (int i = 0; i < 8; ++i) {
-			out[9 + i] = (uint8_t)(cs >> (56 - 8 * i));
-			out[17 + i] = (uint8_t)(cd >> (56 - 8 * i));
-		}
-		pos_sh = 25;
-		n_big = 0;
-	}
-	__syncthreads();
-
-	for (uint32_t t0 = 0; t0 < n; t0 += 256) {
-		const uint32_t j = t0 + tid;
-		const bool valid = j < n;
-		uint32_t cv = 0, cr = 0, cl = 0;
-		uint64_t prev = 0;
-		if (valid) {
-			cv = rec[W * j]; cr = rec[W * j + 1]; cl = rec[W * j + 2];
-			if (j > 0) prev = (uint64_t)rec[W * (j - 1)] + rec[W * (j - 1) + 2];
-		}
-		const uint64_t gap = valid ? cv - prev : 0;
-		const uint64_t sz = valid ? 13 + (gap ? 9 + gap : 0) : 0;
-		scan[tid] = sz;
-		__syncthreads();
-		for (uint32_t d = 1; d < 256; d <<= 1) {
-			const uint64_t y = tid >= d ? scan[tid - d] : 0;
-			__syncthreads();
-			scan[tid] += y;
-			__syncthreads();
-		}
-		const uint64_t pos = pos_sh;
-		const uint64_t S = scan[255];
-		const uint64_t my = scan[tid] - sz;
-		if (S <= kSerStage) {
-			// ── assemble the tile in LDS ──
-			if (valid) {
-				uint8_t* o = stage + my;
-				if (gap) {
-					o[0] = 2;
-					put_u32be_lds(o + 1, (uint32_t)prev);
-					put_u32be_lds(o + 5, (uint32_t)gap);
-					if (gap <= 64) {
-						for (uint32_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
-					} else {
-						const uint32_t b = atomicAdd(&n_big, 1u);
-						big_dst[b] = (uint32_t)(my + 9);
-						big_src[b] = (uint32_t)prev;
-						big_len[b] = (uint32_t)gap;
-					}
-					o += 9 + gap;
-				}
-				o[0] = 1;
-				put_u32be_lds(o + 1, cr);
-				put_u32be_lds(o + 5, cv);
-				put_u32be_lds(o + 9, cl);
-			}
-			__syncthreads();
-			const uint32_t nb = n_big;
-			for (uint32_t b = 0; b < nb; ++b) {
-				uint8_t* d = stage + big_dst[b];
-				const uint8_t* src = V + big_src[b];
-				for (uint32_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
-			}
-			__syncthreads();
-			// ── flush: head bytes to a dword boundary, dwords, tail bytes ──
-			uint8_t* dst = out + pos;
-			const uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
-			const uint32_t Sh = (uint32_t)S;
-			if (tid < head && tid < Sh) dst[tid] = stage[tid];
-			if (Sh > head) {
-				const uint32_t nd = (Sh - head) / 4;
-				uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
-				for (uint32_t k = tid; k < nd; k += 256) {
-					const uint32_t o = head + 4 * k;
-					const uint32_t* w = reinterpret_cast<const uint32_t*>(stage + (o & ~3u));
-					dw[k] = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
-				}
-				const uint32_t tail0 = head + 4 * nd;
-				if (tid < Sh - tail0) dst[tail0 + tid] = stage[tail0 + tid];
-			}
-		} else {
-			// ── direct: each command writes its own bytes ──
-			if (valid) {
-				uint8_t* o = out + pos + my;
-				if (gap) {
-					o[0] = 2;
-					put_u32be(o + 1, (uint32_t)prev);
-					put_u32be(o + 5, (uint32_t)gap);
-					if (gap <= 64) {
-						for (uint64_t i = 0; i < gap; ++i) o[9 + i] = V[prev + i];
-					} else {
-						const uint32_t b = atomicAdd(&n_big, 1u);
-						big_dst[b] = (uint32_t)(pos + my + 9);
-						big_src[b] = (uint32_t)prev;
-						big_len[b] = (uint32_t)gap;
-					}
-					o += 9 + gap;
-				}
-				o[0] = 1;
-				put_u32be(o + 1, cr);
-				put_u32be(o + 5, cv);
-				put_u32be(o + 9, cl);
-			}
-			__syncthreads();
-			const uint32_t nb = n_big;
-			for (uint32_t b = 0; b < nb; ++b) {
-				uint8_t* d = out + big_dst[b];
-				const uint8_t* src = V + big_src[b];
-				for (uint64_t i = tid; i < big_len[b]; i += 256) d[i] = src[i];
-			}
-		}
-		__syncthreads();
-		if (tid == 0) { pos_sh = pos + S; n_big = 0; }
-		__syncthreads();
-	}
-
-	uint64_t pos = pos_sh;
-	const uint64_t last = n ? (uint64_t)rec[W * (n - 1)] + rec[W * (n - 1) + 2] : 0;
-	if (last < vl) {   // trailing ADD
-		const uint64_t len = vl - last;
-		if (tid == 0) {
-			out[pos] = 2;
-			put_u32be(out + pos + 1, (uint32_t)last);
-			put_u32be(out + pos + 5, (uint32_t)len);
-		}
-		for (uint64_t i = tid; i < len; i += 256) out[pos + 9 + i] = V[last + i];
-		pos += 9 + len;
-	}
-	if (tid == 0) {
-		out[pos] = 0;   // END
-		if (pos + 1 != end - base) s.status[pair] = 12;   // DG_ERR_INTERNAL: size pass disagreed
-	}
-}
 
 // ───────────────────────────── CRC-64/XZ ──────────────────────────────────
 //
@@ -408,6 +229,150 @@ __global__ __launch_bounds__(kCrcWideBlock) void crc_segments_wide_kernel(CrcArg
 		const uint64_t c = crc_seg_wave<kCrcLaneBytes, true, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg,
 		                                                     sd.j, tb, a.tables + 8 * 256);
 		if (lane_id() == 0) a.seg_crc[seg] = c;
+	}
+}
+
+// ── row-interleaved segments (coalesced loads) ──
+//
+// The lane-contiguous layout above gives each lane its own 1 KiB of the
+// segment, so every 16-byte load instruction of a wave touches 64 cache
+// lines (the TCP stalls on pending misses; rocprofv3: TCP_PENDING_STALL_CYCLES
+// ~45 % of the kernel at C4).  Here the segment is read as rows of 64 PB-byte
+// pieces, lane l taking piece l of every row, so one load instruction reads
+// 64 PB contiguous bytes.  Lane l folds its column Horner-wise:
+//   A <- sum_j U_j[byte j of (A ^ piece)],
+// U_j = T advanced by (64 PB - 1 - j) bytes — byte j of the piece followed
+// by the rest of its row (the other lanes' pieces) as zeros — so a piece costs
+// PB table lookups like slicing-by-PB, the 64 PB - PB byte advance folded into
+// the tables.  After the last row A_l holds lane l's bytes advanced PB * l
+// bytes too far (the row tail after its piece is 63 PB - PB l bytes, not 63
+// PB); one product by the per-lane constant x^(-8 PB l) fixes that, and the
+// segment's register is the XOR over the lanes (no combine tree).  Zeros
+// before the span leave A at 0; init = ~0 inverts the span's first 8 bytes;
+// the pad after it is undone by the finaliser, as for the layout above.
+//
+// Tables in LDS: NC copies interleaved per entry, entry (j, b) of copy c at
+// tb + 2048 NC j + 8 NC b + 8 c; lane l reads copy l % NC (NC = 4: 8 lanes
+// of a 32-lane group per copy over 8 bank pairs instead of 32 lanes over 32);
+// tables j >= 8 from tbh = tb + 8 * 2048 NC (ds_read offsets are 16-bit).
+template <uint32_t PB, uint32_t NC, int kPf>
+__device__ __forceinline__ uint64_t crc_seg_rows(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
+                                                 uint32_t tb, uint32_t tbh, uint64_t klane) {
+	static_assert(PB == 8 || PB == 16, "piece bytes");
+	constexpr uint32_t RB = 64 * PB, NR = kCrcSegBytes / RB;
+	constexpr uint32_t TS = 2048 * NC, BS = 8 * NC;
+	static_assert(NR % kPf == 0, "rows per prefetch batch");
+	const uint32_t lane = lane_id();
+	const uintptr_t end = start + len;
+	const uintptr_t a0 = start & ~(uintptr_t)15;
+	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
+	const uintptr_t dom = a1 - (uintptr_t)nseg * kCrcSegBytes;   // may wrap below a0
+	const uintptr_t p0 = dom + (uintptr_t)j * kCrcSegBytes + (uintptr_t)lane * PB;
+	// span edges relative to the lane's row-0 piece, clamped so the per-row
+	// tests stay in 32-bit arithmetic
+	auto clamp32 = [](intptr_t v) -> int32_t {
+		return (int32_t)(v < -(intptr_t)RB ? -(intptr_t)RB
+		                 : (v > (intptr_t)(kCrcSegBytes + RB) ? (intptr_t)(kCrcSegBytes + RB) : v));
+	};
+	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)p0);
+	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)p0);
+	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)p0);
+	auto L = [&](uint32_t t, uint32_t b) -> uint64_t {
+		return t < 8 ? ldsq(tb + t * TS + b * BS) : ldsq(tbh + (t - 8) * TS + b * BS);
+	};
+	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+	typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(1))) const v4u gv4;
+	typedef __attribute__((address_space(1))) const v2u gv2;
+	uint64_t A = 0;
+	for (uint32_t r0 = 0; r0 < NR; r0 += kPf) {
+		v4u xs[kPf];
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)((r0 + u) * RB);
+			xs[u] = v4u{0, 0, 0, 0};
+			if (o + (int32_t)PB > z0) {   // pieces wholly before the span: zeros, no load
+				if constexpr (PB == 16) {
+					xs[u] = *reinterpret_cast<gv4*>(p0 + (uintptr_t)(r0 + u) * RB);
+				} else {
+					const v2u h = *reinterpret_cast<gv2*>(p0 + (uintptr_t)(r0 + u) * RB);
+					xs[u].x = h.x;
+					xs[u].y = h.y;
+				}
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)((r0 + u) * RB);
+			v4u x = xs[u];
+			const int32_t f = f0 - o, l = l0 - o;
+			if (__builtin_expect(f > -8 || l < (int32_t)PB, 0)) {   // a span edge in this piece
+				const int fc = max(min(f, 24), -8);
+				const int lc = max(min(l, 24), -8);
+				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
+				lo &= byte_mask(fc, lc);
+				hi &= byte_mask(fc - 8, lc - 8);
+				lo ^= byte_mask(fc, fc + 8);   // init = ~0
+				hi ^= byte_mask(fc - 8, fc);
+				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+			}
+			const uint32_t y0 = (uint32_t)A ^ x.x, y1 = (uint32_t)(A >> 32) ^ x.y;
+			uint64_t n = 0;
+			if constexpr (PB == 16) {   // the lookups that do not wait for A
+				n = L(8, x.z & 0xff) ^ L(9, (x.z >> 8) & 0xff) ^ L(10, (x.z >> 16) & 0xff) ^ L(11, x.z >> 24) ^
+				    L(12, x.w & 0xff) ^ L(13, (x.w >> 8) & 0xff) ^ L(14, (x.w >> 16) & 0xff) ^ L(15, x.w >> 24);
+			}
+			A = n ^ L(0, y0 & 0xff) ^ L(1, (y0 >> 8) & 0xff) ^ L(2, (y0 >> 16) & 0xff) ^ L(3, y0 >> 24) ^
+			    L(4, y1 & 0xff) ^ L(5, (y1 >> 8) & 0xff) ^ L(6, (y1 >> 16) & 0xff) ^ L(7, y1 >> 24);
+		}
+	}
+	uint64_t c = A ? gf2_mulmod(A, klane) : 0ull;
+#pragma unroll
+	for (int d = 32; d >= 1; d >>= 1) {
+		const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c, d, 64);
+		const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), d, 64);
+		c ^= ((uint64_t)hi << 32) | lo;
+	}
+	return uni64(c);
+}
+
+#ifndef DG_CRC_ROWS
+#define DG_CRC_ROWS 3   // bit 0: the wide pass, bit 1: the pass beside another kernel
+#endif
+
+// Wide: 16-byte pieces, 4 table copies (128 KiB), one 1024-thread block per CU.
+__global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
+	extern __shared__ uint64_t TW[];   // 16 tables x 256 x 4 copies
+	for (uint32_t i = threadIdx.x; i < 16 * 256 * 4; i += kCrcWideBlock) TW[i] = a.tables[kCrcRows16 + (i >> 2)];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+	const uint32_t tb = lds_addr(TW) + 8u * (lane & 3u);
+	const uint32_t tbh = tb + 8u * 2048u * 4u;
+	const uint64_t kl = a.tables[kCrcRowK16 + lane];
+	constexpr uint32_t kWaves = kCrcWideBlock / 64;
+	for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_rows<16, 4, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len,
+		                                                       sp.nseg, sd.j, tb, tbh, kl);
+		if (lane == 0) a.seg_crc[seg] = c;
+	}
+}
+
+// Beside another kernel: 8-byte pieces, one table copy (16 KiB).
+__global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
+	__shared__ uint64_t T8[8 * 256];
+	for (uint32_t i = threadIdx.x; i < 8 * 256; i += 256) T8[i] = a.tables[kCrcRows8 + i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+	const uint32_t tb = lds_addr(T8);
+	const uint64_t kl = a.tables[kCrcRowK8 + lane];
+	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs; seg += gridDim.x * kCrcWavesPerBlock) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_rows<8, 1, 8>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j,
+		                                         tb, tb, kl);
+		if (lane == 0) a.seg_crc[seg] = c;
 	}
 }
 
@@ -670,12 +635,6 @@ hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_
 	return hipGetLastError();
 }
 
-hipError_t launch_serialize(const SerArgs& s, hipStream_t st) {
-	if (s.n_pairs == 0) return hipSuccess;
-	hipLaunchKernelGGL(serialize_kernel, dim3(s.n_pairs), dim3(256), 0, st, s);
-	return hipGetLastError();
-}
-
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 	if (s.n_pairs == 0) return hipSuccess;
 	hipLaunchKernelGGL(serialize_wave_kernel, dim3(s.n_pairs), dim3(64), 0, st, s);
@@ -689,14 +648,17 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
 	if (a.n_segs) {
 		const uint32_t blocks = std::min<uint32_t>(n_cu, (a.n_segs + 15) / 16);
-		hipLaunchKernelGGL(crc_segments_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 4 * 256 * 16, st, a);
+		if (DG_CRC_ROWS & 1)
+			hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 16 * 256 * 4, st, a);
+		else
+			hipLaunchKernelGGL(crc_segments_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 4 * 256 * 16, st, a);
 	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
 	return hipGetLastError();
 }
 
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap) {
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, bool rows) {
 	if (a.n_segs) {
 		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
 		static const uint32_t env_cap = [] {
@@ -705,7 +667,10 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap) {
 		}();
 		const uint32_t cap = env_cap ? env_cap : overlap_cap;
 		if (cap && blocks > cap) blocks = cap;
-		hipLaunchKernelGGL(crc_segments_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+		if (rows && (DG_CRC_ROWS & 2))
+			hipLaunchKernelGGL(crc_rows_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+		else
+			hipLaunchKernelGGL(crc_segments_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
