@@ -717,6 +717,9 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		pool = std::max<uint64_t>(1ull << 30, std::min<uint64_t>(resident * per, 4ull << 30));
 	}
 	P->n_tables = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint32_t>(n, 1), pool / per));
+	// the device partitions the pool by XCD (8 per GPU): a multiple of 8
+	// tables, at least 8 where the pool holds them
+	if (pool / per >= 8) P->n_tables = std::max<uint32_t>(8, P->n_tables & ~7u);
 
 	int bad = 0;
 	bad |= P->d_pairs.alloc(sizeof(PairDev) * std::max<uint32_t>(n, 1));

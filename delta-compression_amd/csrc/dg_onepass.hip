@@ -63,7 +63,7 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATCH, P_B_ENTRIES,
        P_B_CHUNKS, P_C_CHUNKS, P_EXTENDS, P_REFILLS, P_T_DIAG, P_T_A, P_T_BC, P_T_EXT, P_T_REFILL,
        P_T_TOTAL, P_B_WALKED, P_T_D1, P_T_D2, P_T_D3, P_T_D4, P_D_MEMBERS, P_D_STEPS, P_T_D3A, P_T_D3B,
-       P_T_TAKE, P_T_RESYNC, P_TAKES, P_RESYNCS, P_T_FINAL, kProfN };
+       P_T_TAKE, P_T_RESYNC, P_TAKES, P_RESYNCS, P_T_FINAL, P_T_C, kProfN };
 __device__ unsigned long long g_onepass_prof[kProfN];
 constexpr uint32_t kPairProfMax = 16384;   // per pair: start, end (realtime), t_bc, exact epochs
 __device__ unsigned long long g_pair_prof[kPairProfMax * 4];
@@ -133,28 +133,35 @@ constexpr uint64_t kTableWaitTicks = 20ull * 100000000ull;   // 20 s
 constexpr int32_t kStatusTablePool = 11;                     // DG_ERR_TABLE_POOL
 constexpr int32_t kStatusInternal = 12;                      // DG_ERR_INTERNAL
 
-__device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t rel) {
-	return ((unsigned long long)tag << 32) | (0xFFFFFFFFu - rel);
+// Table = 2 x qmax entries, HV[s] at 2s and HR[s] at 2s + 1: one 16-byte
+// load at slot s gives both the lookup of a window whose slot is s and the
+// test whether s already has a writer in the window's own table.
+// Entry = tag (16 bits) | step (32 bits) | fingerprint bits 0..15 (the
+// reference's stored-fingerprint test, onepass.c:180-186, without reading the
+// candidate's bytes).  Tags run 1..kTagMax per table; a table whose tags ran
+// out is cleared.  No atomics: global atomics execute at the memory side
+// (~10x a plain access here); the first writer of a slot is the only writer,
+// found from the slot's entry (an earlier chunk) and a duplicate scan of the
+// chunk's lanes.
+constexpr uint32_t kTagMax = 0xFFFFu;
+
+__device__ __forceinline__ unsigned long long tab_key(uint32_t tag, uint32_t step, uint32_t fp) {
+	return ((unsigned long long)tag << 48) | ((unsigned long long)step << 16) | (fp & 0xFFFFu);
+}
+__device__ __forceinline__ bool tab_cur(unsigned long long e, uint32_t tag) { return (uint32_t)(e >> 48) == tag; }
+__device__ __forceinline__ uint32_t tab_step(unsigned long long e) { return (uint32_t)(e >> 16); }
+__device__ __forceinline__ bool tab_fpok(unsigned long long e, uint32_t fp) {
+	return ((uint32_t)e & 0xFFFFu) == (fp & 0xFFFFu);
 }
 
-__device__ __forceinline__ void tab_insert(unsigned long long* t, uint32_t slot, uint32_t tag,
-                                           uint32_t rel) {
-	if (slot != kSentinel)
-		__hip_atomic_fetch_max(t + slot, tab_key(tag, rel), __ATOMIC_RELAXED,
-		                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// earliest step stored in `slot` under `tag` (<= max_rel), else kSentinel.
-// Read at the memory side (an atomic no-op max): coherent with the inserts
-// whatever XCD last cached the line.
-__device__ __forceinline__ uint32_t tab_lookup(unsigned long long* t, uint32_t slot, uint32_t tag,
-                                               uint32_t max_rel) {
-	if (slot == kSentinel) return kSentinel;
-	const unsigned long long e =
-	    __hip_atomic_fetch_max(t + slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-	if ((uint32_t)(e >> 32) != tag) return kSentinel;
-	const uint32_t rel = 0xFFFFFFFFu - (uint32_t)e;
-	return rel <= max_rel ? rel : kSentinel;
+// The pair (HV[s], HR[s]), read past the L1 (an sc1 load, served by the L2
+// that took the stores).  A table is held by one wave at a time, so one XCD's
+// L2 sees all of a holding's stores and loads; a holding ends with an
+// agent-scope release (L2 write-back) before the lock is freed, so the only
+// stale lines another XCD can hold carry older tags, which no lookup accepts.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u64x2 tab_load(const unsigned long long* t, uint32_t slot) {
+	return __builtin_nontemporal_load((const u64x2*)(t + 2ull * slot));
 }
 
 // ───────────────────────────── byte sources ───────────────────────────────
@@ -211,6 +218,10 @@ constexpr uint32_t kListReuse = DG_LIST_REUSE;   // reuse a cached list with at 
 // look-back choice per round: DPP shifts cost ~6 VALU per step of the
 // longest member, the Bloom filter a fixed ~kBloomBase plus ~10 per member
 constexpr uint32_t kBloomBase = DG_BLOOM_BASE;
+#ifndef DG_BACKOFF_MAX
+#define DG_BACKOFF_MAX 4
+#endif
+constexpr uint32_t kBackoffMax = DG_BACKOFF_MAX;   // tier backoff: at most 2^k - 1 epochs skipped
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
 struct WinSrc {
@@ -680,7 +691,7 @@ struct PairResult {
 template <bool kMembers, class Src, bool kRouted = false>
 __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
-                                             uint32_t* bm) {
+                                             uint32_t* bm, uint32_t* cscr) {
 	const uint32_t lane = lane_id();
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
@@ -695,7 +706,6 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	int32_t tslot = -1;  // table tier state
 	uint32_t tag = 0;
 	unsigned long long* HV = nullptr;
-	unsigned long long* HR = nullptr;
 	// the epoch's last tag goes back with the table, so its next holder
 	// starts above every entry this one wrote
 	auto release_table = [&]() {
@@ -711,6 +721,11 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	bool scanning = vl > 0;
 	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
 	bool skipA = false;         // the epoch is known to be long: phase B from step 0
+	// Backoff of the diagonal batch and of phase A: either only pays when most
+	// epochs resolve there (substitutions); after k failures in a row the next
+	// 2^k - 1 epochs go straight to the next tier (the result is the same, the
+	// tiers only differ in cost)
+	uint32_t diag_miss = 0, diag_skip = 0, a_miss = 0, a_skip = 0;
 
 	// ── member mode (dg_members.hip): verified diagonal members are taken as
 	//    they are, 64 records per pass, chunk after chunk; the epochs below
@@ -866,12 +881,18 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		// the epoch start (the reference keeps scanning the other, :102-104)
 		if (v0 + p > vl || r0 + p > rl) break;
 		if constexpr (Src::kPhaseA) {
-			if (at_mismatch) {
+			const bool try_diag = at_mismatch && diag_skip == 0;
+			if (at_mismatch && !try_diag) --diag_skip;
+			if (try_diag) {
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
 				if (members) nb_note();
 				const auto dg = src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm);
 				const uint32_t f = uni(dg.committed);
 				skipA = f == 0 && uni(dg.long_first) != 0u;
+				// matches that leave the diagonal (insertions, deletions, moved
+				// blocks) make the batch commit nothing: back off exponentially
+				diag_miss = f == 0 ? umin32(diag_miss + 1u, kBackoffMax) : 0u;
+				diag_skip = (1u << diag_miss) - 1u;
 				PROF_ADD(src, P_T_DIAG, PROF_NOW() - td);
 				PROF_ADD(src, P_DIAG_CALLS, 1);
 				PROF_ADD(src, P_DIAG_EPOCHS, f);
@@ -897,6 +918,12 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 		// ── phase A: steps 0..7, four lanes per window ──
 		if constexpr (Src::kPhaseA) if (skipA) {
+			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
+			pw = uni(src.rd4(0, v0));   // V bytes from the epoch start (the ADD payload's head)
+		}
+		if constexpr (Src::kPhaseA) if (!skipA && a_skip) {
+			--a_skip;
+			skipA = true;
 			src.ensure2(v0, r0, 8 + 16 + 8, true, true);
 			pw = uni(src.rd4(0, v0));   // V bytes from the epoch start (the ADD payload's head)
 		}
@@ -948,6 +975,9 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			}
 			PROF_ADD(src, P_T_A, PROF_NOW() - ta);
 			PROF_ADD(src, P_A_MATCH, matched);
+			// epochs longer than 8 steps in a row: phase B from step 0 for a while
+			a_miss = matched ? 0u : umin32(a_miss + 1u, kBackoffMax);
+			a_skip = (1u << a_miss) - 1u;
 			if (!matched && nlive <= 8) break;   // both streams exhausted: scan over
 		}
 
@@ -1034,7 +1064,14 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 					}
 				}
 			} else {
-				// ── phase C: per-pair (tag, earliest step) table in HBM ──
+				// ── phase C: per-pair (tag, earliest step, fingerprint) table in HBM ──
+				// Steps 0 .. 64*kHistChunks-1 stay in registers (their slots in
+				// the phase-B bitmaps); later chunks go to the table.  Per chunk:
+				// one 16-byte load per window slot gives the lookup and the
+				// first-writer test, the chunk's own steps are resolved from
+				// registers (a per-chunk bitmap flags candidates and duplicate
+				// slots), and the chunk's first writers are stored after it.
+				[[maybe_unused]] const uint64_t tc0 = PROF_NOW();
 				if (!in_table) {
 					in_table = true;
 					if (tslot < 0) {
@@ -1042,12 +1079,18 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 						// ends), so the wait always drains; the wall-clock bound
 						// only guarantees every wave an exit.  Running into it is
 						// a pool-capacity condition, reported as such.
+						// Tables are partitioned by XCD (the plan makes n_tables a
+						// multiple of 8): a table's lines are only ever cached in
+						// one L2, so no stale copy survives a tag wrap.
 						uint32_t got = 0xFFFFFFFFu;
 						if (lane == 0) {
-							const uint32_t n = a.n_tables;
+							const uint32_t parts = a.n_tables >= 8u ? 8u : 1u;
+							const uint32_t n = a.n_tables / parts;
+							const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // HW_REG_XCC_ID
+							const uint32_t tbase = (xcc % parts) * n;
 							const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 							for (uint32_t it = 0; got == 0xFFFFFFFFu; ++it) {
-								const uint32_t slx = (pair + it) % n;
+								const uint32_t slx = tbase + (pair + it) % n;
 								if (atomicCAS(&a.table_locks[slx], 0u, 1u) == 0u) {
 									got = slx;
 								} else if ((it % n) == n - 1) {
@@ -1060,46 +1103,121 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 						if (got == 0xFFFFFFFFu) { st = kStatusTablePool; scanning = false; break; }
 						tslot = (int32_t)got;
 						HV = a.tables + (uint64_t)got * 2ull * a.qmax;
-						HR = HV + a.qmax;
 						uint32_t t0 = 0;
 						if (lane == 0)
-							t0 = __hip_atomic_load(&a.table_tags[got], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+							t0 = __hip_atomic_load(&a.table_tags[got], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
 						tag = rdlane(t0, 0);
 					}
-					if (tag == 0xFFFFFFFFu) {   // tag space exhausted: clear the table
-						for (uint64_t i = lane; i < 2ull * a.qmax; i += 64)
-							__hip_atomic_store(HV + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if (tag >= kTagMax) {   // tag space exhausted: clear the table
+						for (uint64_t i = lane; i < 2ull * a.qmax; i += 64) HV[i] = 0ull;
 						vm_drain();
 						tag = 0;
 					}
 					++tag;
-#pragma unroll
-					for (int k = 0; k < kHistChunks; ++k) {
-						tab_insert(HV, hsV[k], tag, 64u * k + lane);
-						tab_insert(HR, hsR[k], tag, 64u * k + lane);
-					}
 				}
-				tab_insert(HV, sV, tag, step);
-				tab_insert(HR, sR, tag, step);
+				vm_drain();   // the previous chunk's stores are in the L2
+				const u64x2 pV = cv ? tab_load(HV, sV) : u64x2{0ull, 0ull};   // HV[sV], HR[sV]
+				const u64x2 pR = cr ? tab_load(HV, sR) : u64x2{0ull, 0ull};   // HV[sR], HR[sR]
+				// per-chunk bitmaps (1024 bits per table): candidates of the
+				// chunk's own steps, and lanes whose slot bit was already set
+				// (a possible duplicate slot among the chunk's lanes)
+				constexpr uint32_t CW = 32;
+				cscr[lane] = 0u;
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+				const uint32_t hv = sV & (32u * CW - 1u), hr = sR & (32u * CW - 1u);
+				const uint32_t oV = cv ? atomicOr(&cscr[hv >> 5], 1u << (hv & 31u)) : 0u;
+				const uint32_t oR = cr ? atomicOr(&cscr[CW + (hr >> 5)], 1u << (hr & 31u)) : 0u;
+				__builtin_amdgcn_s_waitcnt(0xc07f);
+				__builtin_amdgcn_wave_barrier();
+				const bool i1 = cr && ((cscr[hr >> 5] >> (hr & 31u)) & 1u);        // an sV of the chunk may equal sR
+				const bool i2 = cv && ((cscr[CW + (hv >> 5)] >> (hv & 31u)) & 1u);  // an sR of the chunk may equal sV
+				// history: the phase-B bitmaps hold the slots of steps 0 .. 64*kHistChunks-1
+				constexpr uint32_t BW = Src::kBmWords;
+				const bool g1 = cr && bloom_has<BW>(bm, sR);
+				const bool g2 = cv && bloom_has<BW>(bm + BW, sV);
+				// duplicates: every lane whose slot bit was set by another lane
+				// is checked exactly; the others are their slot's only lane
+				bool dupV = false, dupR = false;
+				for (uint64_t w = __ballot(cv && ((oV >> (hv & 31u)) & 1u)); w; w &= w - 1) {
+					const uint32_t L = ffs64(w);
+					const uint64_t m = __ballot(cv && sV == rdlane(sV, L));
+					dupV |= ((m & ~(1ull << ffs64(m))) >> lane) & 1u;
+				}
+				for (uint64_t w = __ballot(cr && ((oR >> (hr & 31u)) & 1u)); w; w &= w - 1) {
+					const uint32_t L = ffs64(w);
+					const uint64_t m = __ballot(cr && sR == rdlane(sR, L));
+					dupR |= ((m & ~(1ull << ffs64(m))) >> lane) & 1u;
+				}
 				vm_drain();
-				const uint32_t c1 = cr ? tab_lookup(HV, sR, tag, step) : kSentinel;
-				const uint32_t c2 = cv ? tab_lookup(HR, sV, tag, step) : kSentinel;
-				uint64_t any = __ballot(c1 != kSentinel || c2 != kSentinel);
-				while (any) {
-					const uint32_t j = ffs64(any);
-					any &= any - 1;
+				// earlier chunks of the table tier (the history, if it has the
+				// slot, is earlier still and takes precedence)
+				const bool x1 = cr && tab_cur(pR.x, tag), x2 = cv && tab_cur(pV.y, tag);
+				const bool f1 = x1 && tab_fpok(pR.x, fRl), f2 = x2 && tab_fpok(pV.y, fVl);
+				const uint32_t r1 = tab_step(pR.x), r2 = tab_step(pV.y);
+				// this chunk's first writers go in (after the lookups' loads)
+				if (cv && !dupV && !tab_cur(pV.x, tag)) HV[2ull * sV] = tab_key(tag, step, fVl);
+				if (cr && !dupR && !tab_cur(pR.y, tag)) HV[2ull * sR + 1] = tab_key(tag, step, fRl);
+				uint64_t walk = __ballot(g1 || f1 || (i1 && !x1) || g2 || f2 || (i2 && !x2));
+				const uint64_t G1 = __ballot(g1), G2 = __ballot(g2), X1 = __ballot(x1), X2 = __ballot(x2);
+				while (walk) {
+					const uint32_t j = ffs64(walk);
+					walk &= walk - 1;
 					const uint32_t t = b0 + j;
-					const uint32_t s1 = rdlane(c1, j);
-					if (s1 != kSentinel) {
-						const uint32_t e = src.extend(v0 + s1, r0 + t, umin32(vl - (v0 + s1), rl - (r0 + t)));
-						if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; break; }
+					// lookup 1: the earliest writer of slotR(t) in HV
+					if (t < nr) {
+						const uint32_t x = rdlane(sR, j);
+						uint32_t s1 = kSentinel;
+						bool ok = false;
+						if ((G1 >> j) & 1u) {
+#pragma unroll
+							for (int k = 0; k < kHistChunks; ++k) {
+								if (s1 == kSentinel) {
+									const uint64_t m = __ballot(hsV[k] == x);
+									if (m) { const uint32_t l = ffs64(m); s1 = 64u * k + l; ok = rdlane(hfV[k], l) == rdlane(fRl, j); }
+								}
+							}
+						}
+						if (s1 == kSentinel && ((X1 >> j) & 1u)) {
+							s1 = rdlane(r1, j);
+							ok = rdlane((uint32_t)f1, j) != 0u;
+						} else if (s1 == kSentinel) {
+							const uint64_t m = __ballot(cv && sV == x) & mask_le(j);
+							if (m) { const uint32_t l = ffs64(m); s1 = b0 + l; ok = rdlane(fVl, l) == rdlane(fRl, j); }
+						}
+						if (ok) {
+							const uint32_t e = src.extend(v0 + s1, r0 + t, umin32(vl - (v0 + s1), rl - (r0 + t)));
+							if (e >= p) { matched = true; vm = v0 + s1; rm = r0 + t; ml = e; break; }
+						}
 					}
-					const uint32_t s2 = rdlane(c2, j);
-					if (s2 != kSentinel) {
-						const uint32_t e = src.extend(v0 + t, r0 + s2, umin32(vl - (v0 + t), rl - (r0 + s2)));
-						if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; break; }
+					// lookup 2: the earliest writer of slotV(t) in HR
+					if (t < nv) {
+						const uint32_t x = rdlane(sV, j);
+						uint32_t s2 = kSentinel;
+						bool ok = false;
+						if ((G2 >> j) & 1u) {
+#pragma unroll
+							for (int k = 0; k < kHistChunks; ++k) {
+								if (s2 == kSentinel) {
+									const uint64_t m = __ballot(hsR[k] == x);
+									if (m) { const uint32_t l = ffs64(m); s2 = 64u * k + l; ok = rdlane(hfR[k], l) == rdlane(fVl, j); }
+								}
+							}
+						}
+						if (s2 == kSentinel && ((X2 >> j) & 1u)) {
+							s2 = rdlane(r2, j);
+							ok = rdlane((uint32_t)f2, j) != 0u;
+						} else if (s2 == kSentinel) {
+							const uint64_t m = __ballot(cr && sR == x) & mask_le(j);
+							if (m) { const uint32_t l = ffs64(m); s2 = b0 + l; ok = rdlane(fRl, l) == rdlane(fVl, j); }
+						}
+						if (ok) {
+							const uint32_t e = src.extend(v0 + t, r0 + s2, umin32(vl - (v0 + t), rl - (r0 + s2)));
+							if (e >= p) { matched = true; vm = v0 + t; rm = r0 + s2; ml = e; break; }
+						}
 					}
 				}
+				if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_C, PROF_NOW() - tc0);
 			}
 		}
 		if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_BC, PROF_NOW() - tb);
@@ -1172,7 +1290,7 @@ template <bool kMembers, bool kRouted = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_kernel(EncodeArgs a) {
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
-	__shared__ uint16_t lcache[kListCap];   // the diagonal batch's mismatch list
+	__shared__ __attribute__((aligned(4))) uint16_t lcache[kListCap];   // the diagonal batch's mismatch list; phase-C chunk bitmaps
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
@@ -1207,7 +1325,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
-	const PairResult res = onepass_pair<kMembers, WinSrc, kRouted>(src, a, pair, pd, pp, 16u, bm);
+	const PairResult res = onepass_pair<kMembers, WinSrc, kRouted>(src, a, pair, pd, pp, 16u, bm, (uint32_t*)lcache);
 #ifdef DG_REFILL_PROF
 	if (lane_id() == 0) {
 		atomicAdd(&g_refill_prof[0], (unsigned long long)src.refill_cycles);
@@ -1245,12 +1363,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 template <int PF>
 __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
 	__shared__ uint32_t bm[128];
+	__shared__ uint32_t cscr[64];   // phase-C chunk bitmaps
 	const uint32_t pair = blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
 	GlobalSrc<PF> src{a.ver + pd.v_off, a.ref + pd.r_off, PF > 0 ? (uint32_t)PF : a.p, a.powc};
-	onepass_pair<false>(src, a, pair, pd, pp, src.p, bm);
+	onepass_pair<false>(src, a, pair, pd, pp, src.p, bm, cscr);
 }
 
 // DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel (A/B builds only)

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 NAMES = ["epochs", "diag_calls", "diag_epochs", "diag_zero", "a_entries", "a_match", "b_entries",
          "b_chunks", "c_chunks", "extends", "refills", "t_diag", "t_a", "t_bc", "t_ext", "t_refill",
          "t_total", "b_walked", "t_d1_list", "t_d2_chain", "t_d3_fp_lookup", "t_d4_resolve", "d_members",
-         "d_steps", "t_d3a_map", "t_d3ab_map_fp", "t_take", "t_resync", "takes", "resyncs", "t_final"]
+         "d_steps", "t_d3a_map", "t_d3ab_map_fp", "t_take", "t_resync", "takes", "resyncs", "t_final", "t_c"]
 
 
 def main():
@@ -33,13 +33,15 @@ def main():
     L_.dg_onepass_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     L_.dg_onepass_prof_reset.argtypes = []
     ctx = dg.Context(0)
+    from bench import OPTS, make_inputs
     npg, L, rate, q, seed = CONFIGS[args.config][:5]
     n = args.pairs or npg
-    ref = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    ver = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    ctx.check(L_.dg_synth_edit_pairs_device(ctx.handle, ref.data_ptr(), ver.data_ptr(), n, L, seed + args.offset,
-                                            int(rate * L + 0.5), None), "synth")
-    plan = dg.EncodePlan(ctx, "onepass", [(i * L, L, i * L, L) for i in range(n)], q=q)
+    stream = torch.cuda.current_stream()
+    ref, ver, layout = make_inputs(dg, ctx, torch, args.config, args.offset, n, stream)
+    members = OPTS.get(args.config, {}).get("members")
+    if members is not None:
+        ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, members)
+    plan = dg.EncodePlan(ctx, "onepass", layout, q=q)
     out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
     offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     st = torch.empty(n, dtype=torch.int32, device="cuda")
