@@ -20,9 +20,11 @@ constexpr uint32_t kCrcSegBytes = 64 * kCrcLaneBytes;   // 64 KiB
 constexpr uint32_t kCrcWavesPerBlock = 4;
 
 // Onepass register history: chunks of 64 steps kept in VGPRs before the
-// epoch spills into a global (slot, tag) table.
-#ifndef DG_HIST_CHUNKS   // tuning knob (make variant): 4 -> 94 VGPRs, 5 waves/SIMD; 8 -> 113, 4 waves
-#define DG_HIST_CHUNKS 4
+// epoch spills into the global table tier.  Round 3 A/B (same box, plain
+// chain 90/94/96 VGPRs, no scratch, 5 waves/SIMD for 5/6/7): c3s 54 / 76 /
+// 105 / 105 GiB/s at 4/5/6/7 chunks, C2 and C3 unchanged; 8 spills.
+#ifndef DG_HIST_CHUNKS   // tuning knob (make variant)
+#define DG_HIST_CHUNKS 6
 #endif
 constexpr int kHistChunks = DG_HIST_CHUNKS;
 

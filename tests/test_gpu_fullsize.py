@@ -275,3 +275,52 @@ def test_table_pool_contention(dg, orc, torch_cuda, mode):
     for i, ((R, V), d) in enumerate(zip(pairs, got)):
         assert d == orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q), i
     ctx.close()
+
+
+def test_table_tag_wrap(dg, orc, torch_cuda):
+    """The table tier's 16-bit epoch tags run out and the tables are cleared:
+    one plan reused 60 times over 64 pairs of ~156 epochs of ~380 steps each
+    (every epoch in the table tier) with an 8-table pool (one table per XCD
+    partition) passes 65535 tags per table; every run's deltas equal the
+    oracle's."""
+    torch = torch_cuda
+    rng = random.Random(4242)
+    pairs = []
+    for _ in range(64):
+        R = rng.randbytes(65536)
+        V, c = bytearray(), 0
+        while c + 340 <= len(R):
+            V += rng.randbytes(380) + R[c + 300:c + 340]   # matched at step ~380 of its epoch
+            c += 340
+        pairs.append((R, bytes(V)))
+    ctx = dg.Context(0)
+    ctx.set_limit(dg.LIMIT_TABLE_POOL_BYTES, 8 * 16 * DEFAULT_Q)
+    ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, dg.MEMBERS_OFF)
+    want = [orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q) for R, V in pairs]
+    rb = b"".join(R for R, _ in pairs)
+    vb = b"".join(V for _, V in pairs)
+    layout, ro, vo = [], 0, 0
+    for R, V in pairs:
+        layout.append((ro, len(R), vo, len(V)))
+        ro += len(R)
+        vo += len(V)
+    ref = torch.frombuffer(bytearray(rb), dtype=torch.uint8).cuda()
+    ver = torch.frombuffer(bytearray(vb), dtype=torch.uint8).cuda()
+    plan = dg.EncodePlan(ctx, "onepass", layout, q=DEFAULT_Q)
+    try:
+        out = torch.empty(plan.output_bound, dtype=torch.uint8, device="cuda")
+        off = torch.empty(len(layout) + 1, dtype=torch.int64, device="cuda")
+        st = torch.empty(len(layout), dtype=torch.int32, device="cuda")
+        for run in range(60):
+            plan.run(ref.data_ptr(), ver.data_ptr(), out.data_ptr(), out.numel(), off.data_ptr(),
+                     st.data_ptr(), ctx.stream)
+            torch.cuda.synchronize()
+            assert int(st.abs().sum()) == 0, (run, st.unique().tolist())
+            if run % 10 == 9 or run < 2:
+                o = off.cpu().tolist()
+                blob = out[:o[-1]].cpu().numpy().tobytes()
+                for i, w in enumerate(want):
+                    assert blob[o[i]:o[i + 1]] == w, (run, i)
+    finally:
+        plan.close()
+        ctx.close()
