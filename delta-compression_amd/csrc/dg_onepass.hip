@@ -63,7 +63,7 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 enum { P_EPOCHS, P_DIAG_CALLS, P_DIAG_EPOCHS, P_DIAG_ZERO, P_A_ENTRIES, P_A_MATCH, P_B_ENTRIES,
        P_B_CHUNKS, P_C_CHUNKS, P_EXTENDS, P_REFILLS, P_T_DIAG, P_T_A, P_T_BC, P_T_EXT, P_T_REFILL,
        P_T_TOTAL, P_B_WALKED, P_T_D1, P_T_D2, P_T_D3, P_T_D4, P_D_MEMBERS, P_D_STEPS, P_T_D3A, P_T_D3B,
-       P_T_TAKE, P_T_RESYNC, P_TAKES, P_RESYNCS, P_T_FINAL, P_T_C, kProfN };
+       P_T_TAKE, P_T_RESYNC, P_TAKES, P_RESYNCS, P_T_FINAL, P_T_C, P_T_B1, P_T_B2, P_T_B3, kProfN };
 __device__ unsigned long long g_onepass_prof[kProfN];
 constexpr uint32_t kPairProfMax = 16384;   // per pair: start, end (realtime), t_bc, exact epochs
 __device__ unsigned long long g_pair_prof[kPairProfMax * 4];
@@ -991,6 +991,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			if (b0 >= nlive) { scanning = false; break; }   // both streams exhausted
 			const uint32_t step = b0 + lane;
 			const bool cv = step < nv, cr = step < nr;
+			[[maybe_unused]] const uint64_t tb1 = PROF_NOW();
 			src.chunk(v0 + b0, r0 + b0, b0 < nv, b0 < nr);
 
 			uint64_t fV = 0, fR = 0;
@@ -998,7 +999,9 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			if (cv) { fV = src.fpV(v0 + step); sV = slot_of(fV, mq, q, qmag); }
 			if (cr) { fR = src.fpR(r0 + step); sR = slot_of(fR, mq, q, qmag); }
 			const uint32_t fVl = (uint32_t)fV, fRl = (uint32_t)fR;
-
+#ifdef DG_ONEPASS_PROF
+			if constexpr (Src::kPhaseA) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); PROF_ADD(src, P_T_B1, PROF_NOW() - tb1); }
+#endif
 			if constexpr (Src::kPhaseA) PROF_ADD(src, c < (uint32_t)kHistChunks ? P_B_CHUNKS : P_C_CHUNKS, 1);
 			if (c < (uint32_t)kHistChunks) {
 #pragma unroll
@@ -1026,6 +1029,8 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				const uint32_t j0 = (Src::kPhaseA && c == 0 && !skipA) ? 8u : 0u;
 				uint64_t walk = (m1 | m2) & ~((1ull << j0) - 1ull);
 				if constexpr (Src::kPhaseA) PROF_ADD(src, P_B_WALKED, __builtin_popcountll(walk));
+				[[maybe_unused]] const uint64_t tb3 = PROF_NOW();
+				if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_B2, tb3 - tb1);
 				while (walk) {
 					const uint32_t j = ffs64(walk);
 					walk &= walk - 1;
@@ -1063,6 +1068,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 						}
 					}
 				}
+				if constexpr (Src::kPhaseA) PROF_ADD(src, P_T_B3, PROF_NOW() - tb3);
 			} else {
 				// ── phase C: per-pair (tag, earliest step, fingerprint) table in HBM ──
 				// Steps 0 .. 64*kHistChunks-1 stay in registers (their slots in

@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 NAMES = ["epochs", "diag_calls", "diag_epochs", "diag_zero", "a_entries", "a_match", "b_entries",
          "b_chunks", "c_chunks", "extends", "refills", "t_diag", "t_a", "t_bc", "t_ext", "t_refill",
          "t_total", "b_walked", "t_d1_list", "t_d2_chain", "t_d3_fp_lookup", "t_d4_resolve", "d_members",
-         "d_steps", "t_d3a_map", "t_d3ab_map_fp", "t_take", "t_resync", "takes", "resyncs", "t_final", "t_c"]
+         "d_steps", "t_d3a_map", "t_d3ab_map_fp", "t_take", "t_resync", "takes", "resyncs", "t_final", "t_c", "t_b1_fp", "t_b2_upto_walk", "t_b3_walk"]
 
 
 def main():
