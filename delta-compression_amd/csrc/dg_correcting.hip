@@ -271,10 +271,10 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
                                                                        uint32_t lds_cap) {
 	__shared__ uint64_t nb[256];   // roll61 table: -x 263^p mod M for the byte leaving the window
 	const uint32_t xcd = blockIdx.x & 7u, i = blockIdx.x >> 3;
-	const uint32_t pair = (i / nchunk) * 8u + xcd, chunk = i % nchunk;
-	if (pair >= a.n_pairs) return;
+	const uint32_t gi = (i / nchunk) * 8u + xcd, chunk = i % nchunk;
+	if (gi >= a.n_gpairs) return;   // (only the pairs whose index is too big for LDS)
+	const uint32_t pair = a.gpairs[gi];
 	const PairPlanDev pp = a.pplan[pair];
-	if (pp.q <= lds_cap) return;   // built in LDS by correcting_build_lds_kernel
 	const PairDev pd = a.pairs[pair];
 	const uint32_t p = a.p;
 	const uint64_t seeds = pd.r_len >= p ? pd.r_len - p + 1 : 0;
@@ -670,6 +670,21 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 // lds_cap: the largest R index (slots) built in one block's LDS, 0 = none;
 // pairs with larger indexes take the memory-atomic build (their tables must
 // have been cleared to ~0 by the caller).  qmin/qmax: index sizes in the batch.
+// empty slots (~0) in the memory-built pairs' R indexes only (the LDS build
+// writes its indexes whole): blockIdx.y = listed pair
+__global__ __launch_bounds__(256) void correcting_clear_kernel(EncodeArgs a) {
+	const uint32_t pair = a.gpairs[blockIdx.y];
+	const PairPlanDev& pp = a.pplan[pair];
+	uint32_t* H = a.ctab + pp.tab_base;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < pp.q; i += (uint64_t)gridDim.x * 256) H[i] = kNone;
+}
+
+hipError_t launch_correcting_clear(const EncodeArgs& a, hipStream_t st) {
+	if (a.n_gpairs == 0) return hipSuccess;
+	hipLaunchKernelGGL(correcting_clear_kernel, dim3(16, a.n_gpairs), dim3(256), 0, st, a);
+	return hipGetLastError();
+}
+
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap,
                              uint64_t qmin, hipEvent_t ev_built, hipEvent_t ev_fork) {
 	(void)p;
@@ -682,12 +697,13 @@ hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, ui
 		else
 			hipLaunchKernelGGL(correcting_build_lds_kernel<false>, dim3(a.n_pairs), dim3(kBuildLdsBlock), tb, st, a, lds_cap);
 	}
-	if (a.max_seeds && a.qmax > lds_cap) {
-		// 1-D grid, XCD-aware: block b runs on XCD b mod 8, which takes the
-		// pairs == b (mod 8) one after another, all of a pair's chunks in a
-		// row, so each XCD's L2 holds the few R indexes its atomics hit
+	if (a.max_seeds && a.n_gpairs) {
+		// 1-D grid over the memory-built pairs, XCD-aware: block b runs on
+		// XCD b mod 8, which takes the listed pairs == b (mod 8) one after
+		// another, all of a pair's chunks in a row, so each XCD's L2 holds the
+		// few R indexes its atomics hit
 		const uint32_t nchunk = (uint32_t)((a.max_seeds + kBuildSeedsPerBlock - 1) / kBuildSeedsPerBlock);
-		const uint64_t blocks = 8ull * ((a.n_pairs + 7) / 8) * nchunk;
+		const uint64_t blocks = 8ull * ((a.n_gpairs + 7) / 8) * nchunk;
 		if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
 		hipLaunchKernelGGL(correcting_build_kernel, dim3((uint32_t)blocks), dim3(kBuildBlock), 0, st, a, nchunk, lds_cap);
 	}

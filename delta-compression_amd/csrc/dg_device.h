@@ -111,6 +111,8 @@ struct EncodeArgs {
 	uint32_t* ctab;            // R index: per pair q x u32 offsets (~0 = empty)
 	uint32_t max_seeds;        // max over pairs of |R| - p + 1
 	uint64_t* kcls;            // per pair: checkpoint class k (correcting.c:131-136), computed once
+	const uint32_t* gpairs;    // the pairs whose R index is built in memory (q > the LDS capacity)
+	uint32_t n_gpairs;
 	uint32_t dbg;              // A/B switches (DG_DEBUG_BITS, A/B builds only), 0 in the product
 	// member mode (onepass16_kernel after the member kernels, dg_members.hip):
 	// verified diagonal members are taken as they are; nullptr = plain chain
@@ -264,6 +266,7 @@ hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, h
 hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 // ev_built, ev_fork (nullable): recorded after the R-index build, before the
 // V scan (stage timing; the fork of V's CRC when the build computes R's)
+hipError_t launch_correcting_clear(const EncodeArgs& a, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
                              hipEvent_t ev_built, hipEvent_t ev_fork);
 hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);

@@ -387,7 +387,8 @@ struct dg_encode_plan {
 	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
-	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls;
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls, d_gpairs;
+	uint32_t n_gpairs = 0;       // correcting: pairs whose R index is built in memory
 	// onepass member mode (dg_members.hip): member arrays share the record
 	// slots' indexing; the verification work queue
 	bool members = false;
@@ -737,6 +738,14 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	bad |= P->d_locks.alloc(4ull * P->n_tables);
 	bad |= P->d_tags.alloc(4ull * P->n_tables);
 	if (algo == DG_ALGO_CORRECTING) {
+		std::vector<uint32_t> gp;
+		for (uint32_t i = 0; i < n; ++i)
+			if (P->pp[i].q > P->corr_lds_cap) gp.push_back(i);
+		P->n_gpairs = (uint32_t)gp.size();
+		bad |= P->d_gpairs.alloc(4ull * std::max<size_t>(gp.size(), 1));
+		if (!bad && !gp.empty() &&
+		    hipMemcpy(P->d_gpairs.p, gp.data(), 4 * gp.size(), hipMemcpyHostToDevice) != hipSuccess)
+			bad = 1;
 		bad |= P->d_ctab.alloc(4ull * std::max<uint64_t>(ctab, 1));
 		bad |= P->d_kcls.alloc(8ull * std::max<uint32_t>(n, 1));
 	}
@@ -1087,7 +1096,9 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			a.max_seeds = (uint32_t)P->max_seeds;
 			// the LDS build writes every slot of every index; the global
 			// build only fills, so its tables start empty (~0)
-			if (P->qmax > P->corr_lds_cap) HIPCHK(ctx, hipMemsetAsync(P->d_ctab.p, 0xFF, 4ull * P->ctab_entries, st));
+			a.gpairs = P->d_gpairs.as<uint32_t>();
+			a.n_gpairs = P->n_gpairs;
+			HIPCHK(ctx, launch_correcting_clear(a, st));
 			if (P->crc_fused) {
 				a.crc_out = P->d_crc.as<uint64_t>();
 				a.crc_tab = ctx->d_crc_tables;
