@@ -404,6 +404,7 @@ struct dg_encode_plan {
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
 	bool crc_wide = false;     // correcting: R's and V's CRC in one wide-table pass before the build
+	bool crc_wide_beside = false;   // ... or forked after the build, beside the V scan
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
@@ -645,21 +646,23 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		int shm = 0;
 		if (hipDeviceGetAttribute(&shm, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device) != hipSuccess)
 			shm = 0;
-		// Correcting plans compute the CRCs in one of three ways (A/B:
-		// DG_CORR_CRC = wide | fused | beside):
-		//   wide   (default) one pass over R and V before the build, with the
-		//          GPU to itself: bank-spread slicing tables in 128 KiB of LDS
-		//          per CU (crc_segments_wide_kernel), ~2 LDS cycles a lookup;
-		//   fused  the LDS build computes R's CRC from the bytes it holds and
-		//          V's runs beside the V scan;
+		// Correcting plans compute the CRCs in one of four ways (A/B:
+		// DG_CORR_CRC = fused | wide | widebeside | beside):
+		//   fused  (default) the LDS build computes R's CRC from the bytes it
+		//          holds and V's runs beside the V scan (C4: 2.77 ms per step);
+		//   wide   one pass over R and V before the build, with the GPU to
+		//          itself: bank-spread slicing tables in 128 KiB of LDS per CU
+		//          (crc_segments_wide_kernel), ~2 LDS cycles a lookup (2.84 ms);
+		//   widebeside  the wide pass forked after the build, beside the V
+		//          scan (2.80 ms: it outlasts the scan);
 		//   beside the onepass arrangement: both CRCs on the side stream
 		//          beside the build (whose 130 KiB-LDS blocks leave it ~1/8 of
 		//          each CU).
 		const char* cm = ab_env("DG_CORR_CRC");
-		int mode = 2;
-		if (cm) mode = !strcmp(cm, "fused") ? 1 : (!strcmp(cm, "beside") ? 0 : 2);
+		int mode = 1;
+		if (cm) mode = !strcmp(cm, "wide") ? 2 : (!strcmp(cm, "beside") ? 0 : (!strcmp(cm, "widebeside") ? 3 : 1));
 		if (algo != DG_ALGO_CORRECTING || !n) mode = 0;
-		if (mode == 2 && shm < 8 * 4 * 256 * 16 + 1024) mode = 0;
+		if ((mode == 2 || mode == 3) && shm < 8 * 4 * 256 * 16 + 1024) mode = 0;
 		// one block's LDS less the 2 KiB roll table, the fused R CRC's tables
 		// (10 KiB) and reduction words, and some slack
 		const int fixed = 2048 + (mode == 1 ? 10240 + 128 : 0) + 256;
@@ -668,7 +671,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		// fused: only R indexes built in LDS compute R's CRC; the others' R
 		// CRCs run in V's pass
 		P->crc_fused = mode == 1 && P->corr_lds_cap && P->qmin <= P->corr_lds_cap;
-		P->crc_wide = mode == 2;
+		P->crc_wide = mode == 2 || mode == 3;
+		P->crc_wide_beside = mode == 3;
 	}
 	if (P->crc_fused) {   // x^(-8 pad) of each R's zero padding to a multiple of 32 KiB
 		uint64_t xm8 = 1ULL << 63;
@@ -995,7 +999,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// forked side stream.  The differencing kernel is enqueued first so its
 	// (long, latency-bound) waves are resident before the CRC waves fill the
 	// issue slots they leave idle.
-	const bool serial = P->serial_crc || P->crc_wide;   // the CRC pass on the run stream, first
+	const bool serial = P->serial_crc || (P->crc_wide && !P->crc_wide_beside);   // the CRC pass on the run stream, first
 	hipStream_t cs = serial ? st : P->side;
 	if (P->timing) P->cur = &P->ev[(size_t)kTimingEvents * (P->runs++ % P->slots)];
 	// event k on stream s: every stage event, or (DG_TIMING_DOMINANT) only
@@ -1106,7 +1110,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			}
 			HIPCHK(ctx, launch_correcting(a, a.p, st, P->corr_lds_cap, P->qmin,
 			                              P->timing && (timing_mask(P) & (1u << 7)) ? P->cur[7] : nullptr,
-			                              P->crc_fused && !serial ? P->ev_fork : nullptr));
+			                              (P->crc_fused || P->crc_wide_beside) && !serial ? P->ev_fork : nullptr));
 		}
 		if (P->algo != DG_ALGO_CORRECTING) HIPCHK(ctx, rec(7, st));
 		HIPCHK(ctx, rec(3, st));
@@ -1116,7 +1120,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	if (serial) {
 		if ((rc = run_crc()) != DG_OK) return rc;
 		if ((rc = run_diff()) != DG_OK) return rc;
-	} else if (P->crc_fused) {
+	} else if (P->crc_fused || P->crc_wide_beside) {
 		// the build writes R's CRC; V's CRC forks after the build (ev_fork,
 		// recorded by launch_correcting) and runs beside the V scan
 		if ((rc = run_diff()) != DG_OK) return rc;
