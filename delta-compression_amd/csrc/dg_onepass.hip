@@ -326,7 +326,14 @@ struct WinSrc {
 	}
 
 	__device__ __forceinline__ uint64_t fp16(uint32_t s, uint32_t x) const {
-		return fp16_dot(rd4(s, x), rd4(s, x + 4), rd4(s, x + 8), rd4(s, x + 12));
+		// the window's 16 bytes as one unaligned ds_read_b128 (gfx950 runs with
+		// unaligned LDS access) instead of eight dword reads and four
+		// alignbytes: C2 1721 -> 1732 GiB/s over 4 x 100 steps on one box
+		typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+		typedef __attribute__((address_space(3))) const u32x4u lds_u32x4u;
+		const uint32_t i = x - (s ? base[1] : base[0]);
+		const u32x4u w = *(lds_u32x4u*)(win + (s ? kWinStride : 0) + i);
+		return fp16_dot(w.x, w.y, w.z, w.w);
 	}
 
 	// windows for a 64-step chunk starting at (vpos, rpos)
