@@ -288,7 +288,7 @@ __device__ __forceinline__ uint64_t put_tail(uint8_t* out, const uint8_t* V, uin
 // Wave-wide serialisation of one pair.  `out` = the pair's first output
 // byte, `size` = its delta size (as accumulated by the differencing), `rec`
 // its COPY records (v, r, len) in V order, `stage` >= kStageBytes of LDS.
-// Returns 0, or 5 when the bytes written disagree with `size`.
+// Returns 0, or 12 (DG_ERR_INTERNAL) when the bytes written disagree with `size`.
 template <uint32_t kStageBytes, int kCmd = 1>
 __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint8_t* V, uint32_t vl,
                                          const uint32_t* rec, uint32_t W, uint32_t n, sw_lds8* stage) {
@@ -303,7 +303,7 @@ __device__ inline int32_t serialize_wave(uint8_t* out, uint64_t size, const uint
 		prev_end = r[0] + r[2];
 	}
 	pos += put_tail(out + pos, V, vl, prev_end);
-	return pos == size ? 0 : 5;
+	return pos == size ? 0 : 12;   // DG_ERR_INTERNAL
 }
 
 }  // namespace dg
