@@ -12,6 +12,8 @@ bash scripts/pmc_traffic.sh r03 c3 member_chunk_kernel > gpurun_out/r03prof/p3.l
 bash scripts/pmc_traffic.sh r03 c4 "correcting_build_lds_kernel|correcting_build_kernel|correcting_scan_kernel" "correcting_build_kernel + correcting_scan_kernel" > gpurun_out/r03prof/p4.log 2>&1 || { echo "pmc c4 failed"; tail -5 gpurun_out/r03prof/p4.log; exit 1; }
 bash scripts/pmc_traffic.sh r03 c4 "correcting_build_lds_kernel|correcting_build_kernel" "correcting_build (LDS and memory-atomic builds)" c4_build > gpurun_out/r03prof/p4b.log 2>&1 || { echo "pmc c4 build failed"; tail -5 gpurun_out/r03prof/p4b.log; exit 1; }
 bash scripts/pmc_traffic.sh r03 c4 correcting_scan_kernel correcting_scan_kernel c4_scan > gpurun_out/r03prof/p4s.log 2>&1 || { echo "pmc c4 scan failed"; tail -5 gpurun_out/r03prof/p4s.log; exit 1; }
+bash scripts/pmc_traffic.sh r03 c3s_chain onepass16_kernel > gpurun_out/r03prof/p3s.log 2>&1 || { echo "pmc c3s failed"; tail -5 gpurun_out/r03prof/p3s.log; exit 1; }
+bash scripts/pmc_traffic.sh r03 c4o_chain onepass16_kernel > gpurun_out/r03prof/p4o.log 2>&1 || { echo "pmc c4o failed"; tail -5 gpurun_out/r03prof/p4o.log; exit 1; }
 bash scripts/pmc_traffic.sh r03 c5 decode_kernel > gpurun_out/r03prof/p5.log 2>&1 || { echo "pmc c5 failed"; tail -5 gpurun_out/r03prof/p5.log; exit 1; }
 bash scripts/pmc_traffic.sh r03 c5o decode_kernel > gpurun_out/r03prof/p5o.log 2>&1 || { echo "pmc c5o failed"; tail -5 gpurun_out/r03prof/p5o.log; exit 1; }
 echo profiles done
