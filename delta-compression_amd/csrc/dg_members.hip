@@ -776,7 +776,8 @@ __device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
 	const uint8_t* V = a.ver + J.v_off;
 #pragma unroll
 	for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
-	F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));   // (slots 0..63 of the chunk's 129)
+	F.r = make_uint4(0u, 0u, 0u, 0u);   // (slots 0..63 of the chunk's 129, only the bulk members')
+	if (lane < F.cnt) F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));
 	F.first = a.mem_s[F.slot0];
 }
 
