@@ -80,6 +80,14 @@ CONFIGS = {
             "onepass"),
     "c4o_chain": (4096, 262144, -50, 1, 0xC4000000,
                   "c4o with the plain per-pair chain forced (DG_LIMIT_ONEPASS_MEMBERS = 2)", "onepass"),
+    # the north star's upper pair size: 1 MiB pairs,
+    # --table-size 1 -> q = next_prime(65536) = 65537 (onepass.c:61-62)
+    "c6": (1024, 1048576, 0.01, 1, 0xC6000000,
+           "1024 x 1 MiB pairs per GPU, 1% edits, onepass, --table-size 1", "onepass"),
+    # C2 at the CLI's default --table-size (q = 1048573, delta.h:21)
+    "c2_defq": (4096, 65536, 0.01, 1048573, 0xC2000000,
+                "C2 (4096 x 64 KiB pairs per GPU, 1% edits) onepass at the default --table-size "
+                "(q = 1048573)", "onepass"),
 }
 # per-config options: shift pairs (percent of edits that are insertions or
 # deletions), the chain mode forced through the context limit, the config
@@ -93,7 +101,7 @@ OPTS = {
 REF_MODE = {"onepass": 1, "correcting": 2, "decode": 12, "decode_correcting": 13}
 # CPU baseline samples (pairs): ~1-3 s per timed repetition of the reference's src/c
 CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024, 4096), "c5o": (128, 1024),
-              "c3s": (32, 256), "c4o": (64, 512)}
+              "c3s": (32, 256), "c4o": (64, 512), "c6": (64, 256), "c2_defq": (1024, 4096)}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -217,6 +225,27 @@ class Rank:
             self.dist.barrier()
 
 
+def job_pair_bytes(dg, ctx, name, total):
+    """|R|+|V| of every pair of the whole job, from the generators' host-side
+    layout (no device bytes): the byte weights rank 0 balances the ranges by
+    (SURVEY 8(e)).  Substitution pairs are all 2L; shift and transposition
+    pairs vary."""
+    npg, L, rate, q, seed_base, desc, algo = CONFIGS[name]
+    indel = OPTS.get(name, {}).get("indel_pct")
+    if indel is None and rate >= 0:
+        return [2 * L] * total
+    import ctypes as C
+    pairs = (dg._lib.Pair * max(total, 1))()
+    rb, vb = C.c_uint64(), C.c_uint64()
+    if indel is not None:
+        ctx.check(dg.lib.dg_synth_shift_pairs_device(ctx.handle, seed_base, total, L, int(rate * L + 0.5), indel,
+                                                     pairs, C.byref(rb), C.byref(vb), None, None, None), "layout")
+    else:
+        ctx.check(dg.lib.dg_synth_transpose_pairs_device(ctx.handle, seed_base, total, L, int(-rate), pairs,
+                                                         C.byref(rb), C.byref(vb), None, None, None), "layout")
+    return [x.r_len + x.v_len for x in pairs[:total]]
+
+
 def make_inputs(dg, ctx, torch, name, lo, n, stream):
     npg, L, rate, q, seed_base, desc, algo = CONFIGS[name]
     indel = OPTS.get(name, {}).get("indel_pct")
@@ -275,7 +304,8 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     if args.pairs:
         npg = args.pairs
     total = npg * R.world
-    ranges = shard.balanced_ranges([1] * total, R.world) if R.rank == 0 else None
+    ranges = (shard.balanced_ranges(job_pair_bytes(dg, ctx, name, total), R.world) if R.world > 1
+              else [(0, total)]) if R.rank == 0 else None
     allr = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")
     lo, hi = allr[R.rank]
     n = hi - lo
@@ -378,6 +408,7 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         "n_gpus": R.world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "untimed_steps": 1 + n_prof + args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -464,7 +495,8 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     if args.pairs:
         npg = args.pairs
     total = npg * R.world
-    ranges = shard.balanced_ranges([1] * total, R.world) if R.rank == 0 else None
+    ranges = (shard.balanced_ranges(job_pair_bytes(dg, ctx, name, total), R.world) if R.world > 1
+              else [(0, total)]) if R.rank == 0 else None
     lo, hi = shard.all_ranges(R.dist, ranges, R.world, R.rank, "cuda")[R.rank]
     n = hi - lo
     ref, ver, layout = make_inputs(dg, ctx, torch, name, lo, n, stream)
@@ -543,6 +575,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
         "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
         "value": round(v_bytes * R.world * args.steps / elapsed / 2**30, 3),
         "unit": "GiB/s", "n_gpus": R.world, "steps": args.steps, "warmup": args.warmup,
+        "untimed_steps": 1 + args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": (f"synthetic ({'C2' if rate >= 0 else 'C4 transposition'} pairs generated on device; "
@@ -597,6 +630,74 @@ def run_config(name, args, R, dg, ctx, shard, stream, cpu=True):
 def add_cpu_baseline(name, line, args, R):
     if R.world == 1 and R.rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(name)
+
+
+# ───────────────────────────── the printed line ─────────────────────────────
+
+LINE_MAX = 4000   # bytes: the driver keeps only the tail of stdout
+
+
+def _cpu_short(cb):
+    if not cb:
+        return None
+    out = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}
+    smp = cb.get("sample", "")
+    out["sample"] = smp.split(" (times")[0][:220]
+    if cb.get("single_thread"):
+        out["single_thread"] = cb["single_thread"]["value"]
+    return out
+
+
+def _roof_short(r):
+    keys = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "avg_launch_ms",
+            "algorithmic_bytes_per_launch", "path_achieved", "path_frac")
+    out = {k: r[k] for k in keys if k in r}
+    if r.get("traffic") and r.get("algorithmic_bytes_per_launch"):
+        out["traffic_ratio"] = round(r["traffic"] / r["algorithmic_bytes_per_launch"], 3)
+    return out
+
+
+def also_entry(line):
+    """One config of the run in a few numbers (the full line is in the file)."""
+    r = line["roofline"]
+    e = {"value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": r.get("avg_launch_ms"),
+         "frac": r.get("frac"), "path_frac": r.get("path_frac")}
+    if r.get("traffic") and r.get("algorithmic_bytes_per_launch"):
+        e["traffic_ratio"] = round(r["traffic"] / r["algorithmic_bytes_per_launch"], 3)
+    cb = line.get("cpu_baseline")
+    if cb:
+        e["cpu"] = cb["value"]
+    if line["metric"] != LINE_METRIC:
+        e["metric"] = "decode" if "decode" in line["metric"] else line["metric"]
+    return e
+
+
+LINE_METRIC = "delta-encode GiB/s (device-resident batched pairs) at 1/2/4/8 MI355X"
+
+
+def compact_line(line, also, full_path):
+    """The headline as the driver parses it: the BASELINE metric on its config
+    with roofline and cpu_baseline, `also` one short object per config,
+    at most LINE_MAX bytes; every other field is in `full_path`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "untimed_steps", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+    out = {k: line[k] for k in keep if k in line}
+    cfg = line["config"]
+    out["config"] = {k: cfg[k] for k in ("workload", "name", "algorithm", "pairs_per_gpu", "pairs_total",
+                                         "pair_bytes", "q", "parallelism") if k in cfg}
+    out["roofline"] = _roof_short(line["roofline"])
+    out["cpu_baseline"] = _cpu_short(line.get("cpu_baseline"))
+    if also:
+        out["also"] = {k: also_entry(v) for k, v in also.items()}
+    out["full"] = full_path
+    txt = json.dumps(out, separators=(",", ":"))
+    for drop in ("path_frac", "kernel_ms", "metric"):   # stay inside the driver's tail
+        if len(txt) <= LINE_MAX:
+            break
+        for e in out.get("also", {}).values():
+            e.pop(drop, None)
+        txt = json.dumps(out, separators=(",", ":"))
+    return txt
 
 
 # ───────────────────────────── launch ───────────────────────────────────────
@@ -663,11 +764,13 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--also", default="c3,c4,c5,c5o,c3s,c3s_chain,c4o,c4o_chain",
+    ap.add_argument("--also", default="c3,c4,c5,c5o,c6,c2_defq,c3s,c3s_chain,c4o,c4o_chain",
                     help="extra configs measured in the same run, reported under 'also' "
                          "('none' to skip)")
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-out", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="where the full detail of every line goes (the printed line is compact)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher/orchestration check on the CPU over gloo (no GPU)")
     args = ap.parse_args()
@@ -715,10 +818,14 @@ def main():
     add_cpu_baseline(args.config, line, args, R)
     for name in extras:
         add_cpu_baseline(name, also[name], args, R)
-    if extras:
-        line["also"] = also
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        full = dict(line, also=also) if extras else line
+        path = args.full_out
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        print(f"bench.py: every field of every line in {path}", file=sys.stderr, flush=True)
+        print(compact_line(line, also if extras else None, os.path.relpath(path, ROOT)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -486,9 +486,9 @@ def decode(R: bytes, delta: bytes, ignore_hash: bool = False,
     out = Buffer()
     rc = lib.dg_decode(ctx.handle, _u8(R), len(R), _u8(delta), len(delta), int(ignore_hash),
                        C.byref(out))
-    ctx.check(rc, "dg_decode")
     res = C.string_at(out.data, out.len) if out.len else b""
     lib.dg_buffer_free(C.byref(out))
+    ctx.check(rc, "dg_decode")
     return res
 
 

@@ -413,9 +413,10 @@ struct dg_encode_plan {
 	// timing
 	bool timing = false;
 	int timing_mode = DG_TIMING_ALL;
-	// timing: `slots` sets of kTimingEvents events, one set per run (ring)
+	// timing: `slots` sets of kTimingEvents events, one set per run (ring);
+	// ev holds ev_sets >= slots sets (never shrunk, only the ring is)
 	std::vector<hipEvent_t> ev;
-	uint32_t slots = 0, runs = 0;
+	uint32_t slots = 0, runs = 0, ev_sets = 0;
 	hipEvent_t* cur = nullptr;   // event set of the run being enqueued
 };
 
@@ -922,19 +923,24 @@ static uint32_t timing_mask(const dg_encode_plan_t* P) {
 int dg_encode_plan_set_timing(dg_encode_plan_t* P, int slots) {
 	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
 	hipSetDevice(P->ctx->device);
-	if ((uint32_t)slots > P->slots) {
+	if ((uint32_t)slots > P->ev_sets) {
 		for (auto& e : P->ev) hipEventDestroy(e);
 		P->ev.assign((size_t)kTimingEvents * slots, nullptr);
+		P->ev_sets = P->slots = 0;
 		for (auto& e : P->ev)
 			// timing only: no system-scope fence when the event is recorded
 			// (a cache writeback + invalidate per event slowed the timed
 			// steps by 15 %: C2 0.335 -> 0.391 ms with two events per step)
 			if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
 				e = nullptr;
+				P->timing = false;
 				return set_err(P->ctx, DG_ERR_HIP, "hipEventCreate failed");
 			}
-		P->slots = (uint32_t)slots;
+		P->ev_sets = (uint32_t)slots;
 	}
+	// the ring is exactly `slots` runs long, so stage_times averages the
+	// last `slots` runs even after a longer ring was set before
+	P->slots = (uint32_t)slots;
 	P->timing = slots > 0;
 	P->runs = 0;
 	return DG_OK;
@@ -1253,11 +1259,14 @@ struct dg_decode_plan {
 	uint32_t n = 0;
 	int ignore_hash = 0;
 	DevBuf d_desc;   // the decode kernel computes and checks both CRCs itself
-	// byte extents the streams touch in each arena (run rejects overlaps)
+	// byte extents the streams touch in each arena (run rejects overlaps),
+	// and the intervals themselves, sorted and merged per arena (the exact
+	// check when the extents of the arenas overlap)
 	uint64_t ref_end = 0, delta_end = 0, out_end = 0;
+	std::vector<std::pair<uint64_t, uint64_t>> iv_ref, iv_delta, iv_out;
 	bool timing = false;
 	std::vector<hipEvent_t> ev;
-	uint32_t slots = 0, runs = 0;
+	uint32_t slots = 0, runs = 0, ev_sets = 0;   // ring length; event sets allocated
 };
 
 namespace {
@@ -1286,6 +1295,18 @@ int dg_decode_plan_create(dg_context_t* ctx, const dg_decode_desc_t* descs, uint
 		P->ref_end = std::max(P->ref_end, descs[i].ref_off + descs[i].ref_len);
 		P->delta_end = std::max(P->delta_end, descs[i].delta_off + descs[i].delta_len);
 		P->out_end = std::max(P->out_end, descs[i].out_off + descs[i].out_cap);
+		if (descs[i].ref_len) P->iv_ref.push_back({descs[i].ref_off, descs[i].ref_off + descs[i].ref_len});
+		if (descs[i].delta_len) P->iv_delta.push_back({descs[i].delta_off, descs[i].delta_off + descs[i].delta_len});
+		if (descs[i].out_cap) P->iv_out.push_back({descs[i].out_off, descs[i].out_off + descs[i].out_cap});
+	}
+	for (auto* iv : {&P->iv_ref, &P->iv_delta, &P->iv_out}) {
+		std::sort(iv->begin(), iv->end());
+		size_t k = 0;
+		for (const auto& x : *iv) {
+			if (k && x.first <= (*iv)[k - 1].second) (*iv)[k - 1].second = std::max((*iv)[k - 1].second, x.second);
+			else (*iv)[k++] = x;
+		}
+		iv->resize(k);
 	}
 	const size_t nn = std::max<size_t>(n, 1);
 	if (P->d_desc.alloc(sizeof(dg_decode_desc_t) * nn)) {
@@ -1307,19 +1328,22 @@ int dg_decode_plan_create(dg_context_t* ctx, const dg_decode_desc_t* descs, uint
 int dg_decode_plan_set_timing(dg_decode_plan_t* P, int slots) {
 	if (!P || slots < 0) return DG_ERR_INVALID_ARG;
 	hipSetDevice(P->ctx->device);
-	if ((uint32_t)slots > P->slots) {
+	if ((uint32_t)slots > P->ev_sets) {
 		for (auto& e : P->ev) hipEventDestroy(e);
 		P->ev.assign((size_t)kDecEvents * slots, nullptr);
+		P->ev_sets = P->slots = 0;
 		for (auto& e : P->ev)
 			// timing only: no system-scope fence when the event is recorded
 			// (a cache writeback + invalidate per event slowed the timed
 			// steps by 15 %: C2 0.335 -> 0.391 ms with two events per step)
 			if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
 				e = nullptr;
+				P->timing = false;
 				return set_err(P->ctx, DG_ERR_HIP, "hipEventCreate failed");
 			}
-		P->slots = (uint32_t)slots;
+		P->ev_sets = (uint32_t)slots;
 	}
+	P->slots = (uint32_t)slots;   // the ring: exactly the last `slots` runs
 	P->timing = slots > 0;
 	P->runs = 0;
 	return DG_OK;
@@ -1366,8 +1390,23 @@ int dg_decode_plan_run(dg_decode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
 			return na && nb && x < y + nb && y < x + na;
 		};
-		if (overlap(d_out, P->out_end, d_ref, P->ref_end) || overlap(d_out, P->out_end, d_delta, P->delta_end))
-			return set_err(ctx, DG_ERR_INVALID_ARG, "the output arena overlaps the reference or delta arena");
+		// the exact test (only when the extents overlap): the merged output
+		// intervals against the merged reference / delta intervals, one sweep
+		auto named_overlap = [&](const void* b, const std::vector<std::pair<uint64_t, uint64_t>>& ivb) {
+			const uintptr_t xo = (uintptr_t)d_out, xb = (uintptr_t)b;
+			size_t i = 0, j = 0;
+			while (i < P->iv_out.size() && j < ivb.size()) {
+				const uintptr_t a0 = xo + P->iv_out[i].first, a1 = xo + P->iv_out[i].second;
+				const uintptr_t b0 = xb + ivb[j].first, b1 = xb + ivb[j].second;
+				if (a0 < b1 && b0 < a1) return true;
+				if (a1 <= b1) ++i;
+				else ++j;
+			}
+			return false;
+		};
+		if ((overlap(d_out, P->out_end, d_ref, P->ref_end) && named_overlap(d_ref, P->iv_ref)) ||
+		    (overlap(d_out, P->out_end, d_delta, P->delta_end) && named_overlap(d_delta, P->iv_delta)))
+			return set_err(ctx, DG_ERR_INVALID_ARG, "the output bytes overlap the reference or delta bytes");
 	}
 	hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
 	hipEvent_t* ev = nullptr;

@@ -340,7 +340,8 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 			full = true;
 			for (uint32_t k = 0; k < m; ++k) {
 				out_offsets[sl.p0 + k + 1] = out_pos;
-				if (status) status[sl.p0 + k] = DG_ERR_CAPACITY;
+				// a pair the device already failed keeps its own status
+				if (status) status[sl.p0 + k] = st[k] != DG_OK ? st[k] : DG_ERR_CAPACITY;
 			}
 			return DG_OK;
 		}
@@ -705,7 +706,9 @@ extern "C" int dg_decode(dg_context_t* ctx, const uint8_t* r, size_t r_len, cons
 	if (rc) return rc;
 	int32_t s = 0;
 	if (hipMemcpy(&s, d_st.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return DG_ERR_HIP;
-	if (s) return s;
+	// a failed output CRC still hands back the output: the reference writes
+	// the file before its post-check fails (main.c:374-383)
+	if (s && s != DG_ERR_DST_CRC) return s;
 	if (vsize && (hipMemcpyAsync(h_o.p, d_o.p, vsize, hipMemcpyDeviceToHost, st) != hipSuccess ||
 	              hipStreamSynchronize(st) != hipSuccess))
 		return DG_ERR_HIP;
@@ -713,5 +716,5 @@ extern "C" int dg_decode(dg_context_t* ctx, const uint8_t* r, size_t r_len, cons
 	if (!out->data) return DG_ERR_NOMEM;
 	if (vsize) memcpy(out->data, h_o.p, vsize);
 	out->len = vsize;
-	return DG_OK;
+	return s;
 }

@@ -176,6 +176,7 @@ struct GlobalSrc {
 	uint32_t p;
 	const uint64_t* powc;
 	__device__ void chunk(uint32_t, uint32_t, bool, bool) {}
+	__device__ void drop_list() {}
 	__device__ uint64_t fpV(uint32_t pos) { return window_fp<PF>(V + pos, p, powc); }
 	__device__ uint64_t fpR(uint32_t pos) { return window_fp<PF>(R + pos, p, powc); }
 	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
@@ -239,6 +240,8 @@ struct WinSrc {
 	uint16_t* lc;            // kListCap entries
 	uint32_t lc_base = 0, lc_diag = 0, lc_n = 0;
 	bool lc_end = false;     // the list ends with the stream-end entry
+	// phase C reuses lc's LDS for its per-chunk bitmaps: the list is gone
+	__device__ void drop_list() { lc_n = 0; }
 	PROF_DECL
 #ifdef DG_REFILL_PROF
 	uint64_t refill_cycles = 0;
@@ -1087,6 +1090,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				[[maybe_unused]] const uint64_t tc0 = PROF_NOW();
 				if (!in_table) {
 					in_table = true;
+					src.drop_list();
 					if (tslot < 0) {
 						// Holders never wait (a table is released when its pair
 						// ends), so the wait always drains; the wall-clock bound

@@ -296,7 +296,10 @@ int dg_crc64_xz_batch_device(dg_context_t *ctx, const uint8_t *d_arena,
 
 /* Decode one delta against R (host buffers).  Returns DG_OK,
  * DG_ERR_MALFORMED, DG_ERR_SRC_CRC or DG_ERR_DST_CRC (the reference's exit
- * paths); ignore_hash skips both CRC checks (main.c:330-333). */
+ * paths); ignore_hash skips both CRC checks (main.c:330-333).  On DG_OK and
+ * on DG_ERR_DST_CRC, *out holds the decoded bytes (the reference writes the
+ * output before its post-check fails, main.c:374-383): free it with
+ * dg_buffer_free in both cases. */
 int dg_decode(dg_context_t *ctx, const uint8_t *r, size_t r_len,
               const uint8_t *delta, size_t delta_len, int ignore_hash,
               dg_buffer_t *out);

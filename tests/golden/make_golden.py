@@ -62,6 +62,9 @@ def main():
         ("c2", 0xC2000000, 65536, 655, 1, 8),
         ("c2_default_q", 0xC2000000, 65536, 655, 1048573, 2),
         ("c3", 0xC3000000, 262144, 26214, 1, 4),
+        # the north star's upper pair size: 1 MiB, 1 %, q = next_prime(65536) = 65537
+        ("c6", 0xC6000000, 1048576, 10486, 1, 4),
+        ("c6_default_q", 0xC6000000, 1048576, 10486, 1048573, 1),
     ]
     for tag, seed, L, ne, q, count in synth:
         for i in range(count):

@@ -49,3 +49,24 @@ def test_bench_refuses_ab_switches():
                        env=_env(DG_SERIAL_CRC="1"), capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "refusing" in (r.stderr + r.stdout)
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_compact_line_fits_driver_tail():
+    """The printed line stays <= 4 KB with every config under `also`
+    (a 20 KB line overflowed the driver's stdout tail)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    full = json.load(open(os.path.join(ROOT, "profiles", "r03_bench_default_final.json")))
+    also = full.pop("also")
+    names = [n for n in bench.CONFIGS if n != "c2"]
+    also = {n: dict(also[n if n in also else "c3"]) for n in names}
+    txt = bench.compact_line(full, also, "gpurun_out/bench_full.json")
+    assert len(txt) <= bench.LINE_MAX
+    d = json.loads(txt)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "roofline", "cpu_baseline"):
+        assert k in d
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in d["roofline"]
+    assert d["cpu_baseline"]["cores"] and d["cpu_baseline"]["kind"] == "reference"
+    assert set(d["also"]) == set(names)
+    assert all("value" in e and "frac" in e for e in d["also"].values())

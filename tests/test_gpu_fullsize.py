@@ -104,6 +104,84 @@ def test_c3_full_batch(dg, ctx_mode, orc, torch_cuda):
     torch.cuda.empty_cache()
 
 
+def _decode_all_back(dg, ctx, torch, ref, ver, out, offs, n, L):
+    """Every pair's delta decoded back to V in one device batch (CRCs checked there)."""
+    descs = (dg._lib.DecodeDesc * n)(*[
+        dg._lib.DecodeDesc(i * L, L, offs[i], offs[i + 1] - offs[i], i * L, L) for i in range(n)])
+    dec = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dlen = torch.empty(n, dtype=torch.int64, device="cuda")
+    dst = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.check(dg.lib.dg_decode_batch_device(ctx.handle, ref.data_ptr(), out.data_ptr(), descs, n, 0,
+                                            dec.data_ptr(), dlen.data_ptr(), dst.data_ptr(), None),
+              "decode batch")
+    torch.cuda.synchronize()
+    assert int(dst.abs().sum()) == 0
+    assert bool((dlen == L).all())
+    assert bool(torch.equal(dec, ver))
+
+
+def test_c6_full_batch(dg, ctx_mode, orc, torch_cuda):
+    """The north star's upper pair size: the whole
+    1024 x 1 MiB, 1%-edit batch the bench's c6 line times, at --table-size 1
+    (q = next_prime(65536) = 65537, onepass.c:61-62), in both chain modes:
+    pairs 0..3 equal the reference-minted goldens, a spread sample equals
+    the oracle, every pair decodes back to V on the device."""
+    torch = torch_cuda
+    ctx = ctx_mode
+    n, L, seed, ne = 1024, 1 << 20, 0xC6000000, 10486
+    ref, ver = _synth(dg, ctx, torch, n, L, ne, seed)
+    layout = [(i * L, L, i * L, L) for i in range(n)]
+    plan = dg.EncodePlan(ctx, "onepass", layout, q=1)
+    assert plan.table_size(0) == 65537
+    plan.close()
+    out, off, st = _encode(dg, ctx, torch, ref, ver, layout, q=1)
+    assert int((st != 0).sum()) == 0, st.unique().tolist()
+    offs = off.cpu().tolist()
+    assert offs[0] == 0 and all(offs[i] < offs[i + 1] for i in range(n))
+
+    def delta(i):
+        return bytes(out[offs[i]:offs[i + 1]].cpu().numpy())
+
+    for i in range(4):
+        g = _golden(f"c6_{i}")
+        assert g["seed"] == seed + i and g["n_edits"] == ne and g["q"] == 1
+        assert hashlib.sha256(delta(i)).hexdigest() == g["delta_sha256"], i
+    for i in [5, 511, 512, 777, n - 1]:
+        R, V = orc.synth_pair(seed + i, L, ne)
+        assert delta(i) == orc.encode(ONEPASS, R, V, p=16, q=1), i
+    _decode_all_back(dg, ctx, torch, ref, ver, out, offs, n, L)
+    del ref, ver, out
+    torch.cuda.empty_cache()
+
+
+def test_c2_default_q_full_batch(dg, ctx, orc, torch_cuda):
+    """C2 at the CLI's default --table-size (q = 1048573, delta.h:21): the
+    whole 4096-pair batch of the bench's c2_defq line, the reference-minted
+    goldens of pairs 0..1, an oracle sample, every pair decoded back."""
+    torch = torch_cuda
+    n, L, seed, ne = 4096, 65536, 0xC2000000, 655
+    ref, ver = _synth(dg, ctx, torch, n, L, ne, seed)
+    layout = [(i * L, L, i * L, L) for i in range(n)]
+    out, off, st = _encode(dg, ctx, torch, ref, ver, layout, q=DEFAULT_Q)
+    assert int((st != 0).sum()) == 0, st.unique().tolist()
+    offs = off.cpu().tolist()
+
+    def delta(i):
+        return bytes(out[offs[i]:offs[i + 1]].cpu().numpy())
+
+    for i in range(2):
+        g = _golden(f"c2_default_q_{i}")
+        assert g["q"] == DEFAULT_Q
+        assert hashlib.sha256(delta(i)).hexdigest() == g["delta_sha256"], i
+    for i in [7, 1000, 2049, n - 1]:
+        R, V = orc.synth_pair(seed + i, L, ne)
+        assert delta(i) == orc.encode(ONEPASS, R, V, p=16, q=DEFAULT_Q), i
+    _decode_all_back(dg, ctx, torch, ref, ver, out, offs, n, L)
+    del ref, ver, out
+    torch.cuda.empty_cache()
+
+
 def test_c5_inplace_full_batch(dg, ctx, orc, torch_cuda):
     import oracle as O
     torch = torch_cuda
