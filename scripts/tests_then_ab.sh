@@ -1,6 +1,6 @@
 #!/bin/bash
 # Parity tests on the product library, then a same-box A/B of variant
-# libraries.  usage: VARIANTS="base x" CONFIGS="c2 c3s_chain" scripts/r03_ab.sh TAG [rounds]
+# libraries.  usage: VARIANTS="base x" CONFIGS="c2 c3s_chain" scripts/tests_then_ab.sh TAG [rounds]
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
