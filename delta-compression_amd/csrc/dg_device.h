@@ -79,7 +79,16 @@ constexpr int kCrcFinX256 = 20, kCrcFinX512 = 21, kCrcFinX48K = 22;   // indices
 constexpr uint32_t kCrcRowsOff = 8 * 256 + (kCrcLevels + kCrcFinTabs) * kCrcNibTabWords;
 constexpr uint32_t kCrcRows16 = kCrcRowsOff, kCrcRows8 = kCrcRowsOff + 16 * 256;
 constexpr uint32_t kCrcRowK16 = kCrcRowsOff + 24 * 256, kCrcRowK8 = kCrcRowK16 + 64;
-constexpr uint32_t kCrcTabWords = kCrcRowK8 + 64;
+// then the five-bit row tables (crc_seg_rows5): F_k[v] = Z^n(v << 5k), k = 0..12,
+// 32 entries (256 B: one LDS row, so a 32-lane ds_read_b64 group never
+// conflicts) -- for 8-byte pieces n = 512; for 16-byte pieces n = 1024 on
+// (A ^ low 8 bytes), then 13 more with n = 1016 on the high 8 bytes
+constexpr uint32_t kCrc5Tabs8 = 13, kCrc5Tabs16 = 26;
+#ifndef DG_CRC5
+#define DG_CRC5 1   // the row passes use the five-bit tables (0: the byte tables)
+#endif
+constexpr uint32_t kCrc5R8 = kCrcRowK8 + 64, kCrc5R16 = kCrc5R8 + 32 * kCrc5Tabs8;
+constexpr uint32_t kCrcTabWords = kCrc5R16 + 32 * kCrc5Tabs16;
 
 
 struct EncodeArgs {

@@ -258,6 +258,26 @@ int dg_context_create(int device, dg_context_t** out) {
 			tab[kCrcRowK8 + l] = z;
 			for (int b = 0; b < 64; ++b) z = gf2_div_x(z);
 		}
+		// five-bit row tables: the images Z^n(2^i) of the 64 register bits
+		// (Z = one zero byte through the register), combined per 5-bit field
+		auto five = [&](uint32_t base, int n) {
+			uint64_t col[64];
+			for (int i = 0; i < 64; ++i) {
+				uint64_t x = 1ULL << i;
+				for (int k = 0; k < n; ++k) x = (x >> 8) ^ tab[x & 0xff];
+				col[i] = x;
+			}
+			for (int k = 0; k < 13; ++k)
+				for (int v = 0; v < 32; ++v) {
+					uint64_t r = 0;
+					for (int b = 0; b < 5; ++b)
+						if (((v >> b) & 1) && 5 * k + b < 64) r ^= col[5 * k + b];
+					tab[base + 32 * k + v] = r;
+				}
+		};
+		five(kCrc5R8, 512);
+		five(kCrc5R16, 1024);
+		five(kCrc5R16 + 32 * 13, 1016);
 	}
 	std::vector<uint64_t> k32(1024);
 	{
@@ -1037,8 +1057,9 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			if (P->crc_wide) HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, cs));
 			// (member plans keep the 8 KiB-LDS lane-contiguous pass: the row pass's
 			// 16 KiB blocks find no room beside the member kernel and trail it)
+			// (five-bit row tables, 3.25 KiB, fit beside it too)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            !P->members));
+			                            DG_CRC5 || !P->members));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;

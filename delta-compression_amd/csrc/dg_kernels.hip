@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dg_device.h"
 #include "dg_devutil.h"
 #include "dg_serialize_wave.h"
@@ -336,13 +338,118 @@ __device__ __forceinline__ uint64_t crc_seg_rows(uintptr_t start, uint64_t len, 
 	return uni64(c);
 }
 
+// ── five-bit row tables ──
+//
+// The same row fold with the 64-bit (A ^ piece) split into 13 five-bit fields
+// instead of 8 bytes: 13 lookups in tables of 32 entries x 8 B = 256 B, one
+// LDS row across all 64 banks.  A ds_read_b64 is serviced in two 32-lane
+// groups; within a group distinct entries of one table sit on distinct bank
+// pairs and equal entries broadcast, so no lookup ever conflicts (random byte
+// indices into a 2 KiB table cost ~3.5 LDS cycles per group).  13 conflict-free
+// lookups per 8 bytes instead of 8 at ~3.5.  Tables at tb (256-byte aligned),
+// table k at tb + 256 k.
+__device__ __forceinline__ uint64_t fold5(uint32_t lo, uint32_t hi, uint32_t tb) {
+	const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 30);   // bits 30..34
+	auto L = [&](uint32_t k, uint32_t f) -> uint64_t { return ldsq(tb + 256u * k + 8u * f); };
+	return L(0, lo & 31u) ^ L(1, __builtin_amdgcn_ubfe(lo, 5, 5)) ^ L(2, __builtin_amdgcn_ubfe(lo, 10, 5)) ^
+	       L(3, __builtin_amdgcn_ubfe(lo, 15, 5)) ^ L(4, __builtin_amdgcn_ubfe(lo, 20, 5)) ^
+	       L(5, __builtin_amdgcn_ubfe(lo, 25, 5)) ^ L(6, mid & 31u) ^ L(7, __builtin_amdgcn_ubfe(hi, 3, 5)) ^
+	       L(8, __builtin_amdgcn_ubfe(hi, 8, 5)) ^ L(9, __builtin_amdgcn_ubfe(hi, 13, 5)) ^
+	       L(10, __builtin_amdgcn_ubfe(hi, 18, 5)) ^ L(11, __builtin_amdgcn_ubfe(hi, 23, 5)) ^ L(12, hi >> 28);
+}
+
+// crc_seg_rows with the five-bit tables (PB = 8: 13 tables; PB = 16: 26, the
+// second 13 for the piece's high 8 bytes, which do not wait for A).  SEG:
+// segment bytes (64 KiB for the encode passes, 16 KiB in the decode kernel).
+template <uint32_t PB, int kPf, uint32_t SEG = kCrcSegBytes>
+__device__ __forceinline__ uint64_t crc_seg_rows5(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
+                                                  uint32_t tb, uint64_t klane) {
+	static_assert(PB == 8 || PB == 16, "piece bytes");
+	constexpr uint32_t RB = 64 * PB, NR = SEG / RB;
+	static_assert(NR % kPf == 0, "rows per prefetch batch");
+	const uint32_t lane = lane_id();
+	const uintptr_t end = start + len;
+	const uintptr_t a0 = start & ~(uintptr_t)15;
+	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
+	const uintptr_t dom = a1 - (uintptr_t)nseg * SEG;   // may wrap below a0
+	const uintptr_t p0 = dom + (uintptr_t)j * SEG + (uintptr_t)lane * PB;
+	auto clamp32 = [](intptr_t v) -> int32_t {
+		return (int32_t)(v < -(intptr_t)RB ? -(intptr_t)RB : (v > (intptr_t)(SEG + RB) ? (intptr_t)(SEG + RB) : v));
+	};
+	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)p0);
+	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)p0);
+	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)p0);
+	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+	typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+	typedef __attribute__((address_space(1))) const v4u gv4;
+	typedef __attribute__((address_space(1))) const v2u gv2;
+	// the pieces in flight: 16 B (PB = 16) or 8 B each
+	typedef typename std::conditional<PB == 16, v4u, v2u>::type piece_t;
+	typedef typename std::conditional<PB == 16, gv4, gv2>::type gpiece_t;
+	uint64_t A = 0;
+	for (uint32_t r0 = 0; r0 < NR; r0 += kPf) {
+		piece_t xs[kPf];
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)((r0 + u) * RB);
+			xs[u] = piece_t{};
+			if (o + (int32_t)PB > z0) xs[u] = *reinterpret_cast<gpiece_t*>(p0 + (uintptr_t)(r0 + u) * RB);
+		}
+#pragma unroll
+		for (int u = 0; u < kPf; ++u) {
+			const int32_t o = (int32_t)((r0 + u) * RB);
+			v4u x;
+			if constexpr (PB == 16) x = xs[u];
+			else x = v4u{xs[u].x, xs[u].y, 0u, 0u};
+			const int32_t f = f0 - o, l = l0 - o;
+			if (__builtin_expect(f > -8 || l < (int32_t)PB, 0)) {
+				const int fc = max(min(f, 24), -8);
+				const int lc = max(min(l, 24), -8);
+				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
+				lo &= byte_mask(fc, lc);
+				hi &= byte_mask(fc - 8, lc - 8);
+				lo ^= byte_mask(fc, fc + 8);   // init = ~0
+				hi ^= byte_mask(fc - 8, fc);
+				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+			}
+			uint64_t n = 0;
+			if constexpr (PB == 16) n = fold5(x.z, x.w, tb + 256u * 13u);
+			A = n ^ fold5((uint32_t)A ^ x.x, (uint32_t)(A >> 32) ^ x.y, tb);
+		}
+	}
+	uint64_t c = A ? gf2_mulmod(A, klane) : 0ull;
+#pragma unroll
+	for (int d = 32; d >= 1; d >>= 1) {
+		const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c, d, 64);
+		const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), d, 64);
+		c ^= ((uint64_t)hi << 32) | lo;
+	}
+	return uni64(c);
+}
+
 #ifndef DG_CRC_ROWS
 #define DG_CRC_ROWS 3   // bit 0: the wide pass, bit 1: the pass beside another kernel
 #endif
 
-// Wide: 16-byte pieces, 4 table copies (128 KiB), one 1024-thread block per CU.
+// Wide: 16-byte pieces, 4 table copies (128 KiB), one 1024-thread block per CU
+// (five-bit tables: 26 x 256 B, conflict-free, no copies).
 __global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
 	extern __shared__ uint64_t TW[];   // 16 tables x 256 x 4 copies
+	if constexpr (DG_CRC5) {
+		for (uint32_t i = threadIdx.x; i < 32 * kCrc5Tabs16; i += kCrcWideBlock) TW[i] = a.tables[kCrc5R16 + i];
+		__syncthreads();
+		const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+		const uint64_t kl = a.tables[kCrcRowK16 + lane];
+		constexpr uint32_t kWaves = kCrcWideBlock / 64;
+		for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
+			const CrcSegDev sd = a.segs[seg];
+			const CrcSpanDev sp = a.spans[sd.span];
+			const uint64_t c = crc_seg_rows5<16, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len,
+			                                                     sp.nseg, sd.j, lds_addr(TW), kl);
+			if (lane == 0) a.seg_crc[seg] = c;
+		}
+		return;
+	}
 	for (uint32_t i = threadIdx.x; i < 16 * 256 * 4; i += kCrcWideBlock) TW[i] = a.tables[kCrcRows16 + (i >> 2)];
 	__syncthreads();
 	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
@@ -359,8 +466,24 @@ __global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a)
 	}
 }
 
-// Beside another kernel: 8-byte pieces, one table copy (16 KiB).
+// Beside another kernel: 8-byte pieces, one table copy (16 KiB; five-bit
+// tables: 3.25 KiB).
 __global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
+	if constexpr (DG_CRC5) {
+		__shared__ __attribute__((aligned(256))) uint64_t T5[32 * kCrc5Tabs8];
+		for (uint32_t i = threadIdx.x; i < 32 * kCrc5Tabs8; i += 256) T5[i] = a.tables[kCrc5R8 + i];
+		__syncthreads();
+		const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+		const uint64_t kl = a.tables[kCrcRowK8 + lane];
+		for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs; seg += gridDim.x * kCrcWavesPerBlock) {
+			const CrcSegDev sd = a.segs[seg];
+			const CrcSpanDev sp = a.spans[sd.span];
+			const uint64_t c = crc_seg_rows5<8, 4>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j,
+			                                       lds_addr(T5), kl);
+			if (lane == 0) a.seg_crc[seg] = c;
+		}
+		return;
+	}
 	__shared__ uint64_t T8[8 * 256];
 	for (uint32_t i = threadIdx.x; i < 8 * 256; i += 256) T8[i] = a.tables[kCrcRows8 + i];
 	__syncthreads();
@@ -649,7 +772,8 @@ hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
 	if (a.n_segs) {
 		const uint32_t blocks = std::min<uint32_t>(n_cu, (a.n_segs + 15) / 16);
 		if (DG_CRC_ROWS & 1)
-			hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 16 * 256 * 4, st, a);
+			hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock),
+			                   DG_CRC5 ? 256ull * kCrc5Tabs16 : 8ull * 16 * 256 * 4, st, a);
 		else
 			hipLaunchKernelGGL(crc_segments_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 4 * 256 * 16, st, a);
 	}
@@ -1540,6 +1664,18 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		block_sync_global();   // every wave's output stores before any CRC read
 		const uint64_t* Lv = a.tables + 8 * 256;
 		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
+#if DG_CRC5
+		// LDS (the dead doubling arrays): the five-bit row tables (3.25 KiB,
+		// 256-byte aligned) and x^(8 * 64 KiB); 16 KiB segments read as rows
+		// of 64 x 8 bytes (coalesced), conflict-free lookups
+		const uint32_t t5 = (lds_addr(NX) + 255u) & ~255u;
+		uint64_t* T5 = reinterpret_cast<uint64_t*>(NX) + (t5 - lds_addr(NX)) / 8;
+		uint64_t* TK = T5 + 32 * kCrc5Tabs8;
+		static_assert(8 * (32 * kCrc5Tabs8 + kCrcNibTabWords) + 256 <= sizeof(NX), "CRC tables fit NX");
+		for (uint32_t k = tid; k < 32 * kCrc5Tabs8; k += kDecBlock) T5[k] = a.tables[kCrc5R8 + k];
+		for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
+		const uint64_t klane = a.tables[kCrcRowK8 + lane];
+#else
 		// LDS (the dead doubling arrays, 22 of 24 KiB): the slicing-by-4
 		// tables, the tree's levels x^(8 * 256 * 2^l) and x^(8 * 64 KiB)
 		uint64_t* TS = reinterpret_cast<uint64_t*>(NX);
@@ -1555,6 +1691,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			                                      : KF;   // x^(8 * 64 KiB)
 			TT[k] = src[e];
 		}
+#endif
 		__syncthreads();
 		const uintptr_t sa[2] = {(uintptr_t)R, (uintptr_t)O};
 		const uint64_t sl[2] = {rl, vsize};
@@ -1565,7 +1702,11 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			if (sl[sp] >= 8) {
 				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
+#if DG_CRC5
+					const uint64_t c = crc_seg_rows5<8, 4, kDecCrcSeg>(sa[sp], sl[sp], nseg, j, t5, klane);
+#else
 					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, lds_addr(TS), TT);
+#endif
 					acc = (last != ~0u ? mul_nib(acc, TK) : 0ull) ^ c;   // TK: x^(8 * 64 KiB) = 4 segments
 					last = j;
 				}

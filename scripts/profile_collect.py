@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Collect one profile session (scripts/profile_round.sh TAG, merged back
+under gpurun_out/TAG) into profiles/:
+
+  profiles/TAG_kernel_stats_<cfg>.csv   rocprofv3 --stats of the config run alone
+  profiles/TAG_bench_<cfg>.json         the bench line of that same run
+  profiles/TAG_pmc_calib.json           FETCH_SIZE / WRITE_SIZE per access class
+  profiles/TAG_pmc_traffic_<cfg>.json   HBM bytes per launch of the dominant kernel(s)
+  profiles/TAG_rooflines.md             HIP-event vs rocprof average per config
+
+usage: scripts/profile_collect.py TAG
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KNOWN = {   # pmc_calib.cpp: bytes each kernel moves per launch (2 GiB buffers, 16 Mi lines)
+    "stream16": 2 << 30, "dma16": 2 << 30, "rand16": (16 << 20) * 16, "rand4": (16 << 20) * 4,
+    "store16": 2 << 30, "store16r": (16 << 20) * 16,
+}
+# the dominant kernel(s) of each line, as bench.py names them, and the
+# rocprof names that make them up (one launch of each per step)
+DOMINANT = {
+    "onepass16_kernel": [r"onepass16_kernel<false, false>"],
+    "member_chunk_kernel": [r"member_chunk_kernel"],
+    "onepass16_kernel (member chain + routed plain chain)": [r"onepass16_kernel<true, false>",
+                                                             r"onepass16_kernel<false, true>"],
+    "correcting_build_kernel + correcting_scan_kernel": [r"correcting_build_lds_kernel", r"correcting_build_kernel",
+                                                         r"correcting_scan_kernel"],
+    "decode_kernel": [r"decode_kernel"],
+}
+# FETCH class of each dominant kernel's reads (pmc_calib factors apply per class)
+FETCH_CLASS = {"onepass16_kernel": "dma16", "member_chunk_kernel": "dma16", "decode_kernel": "stream16",
+               "correcting_build_kernel + correcting_scan_kernel": "stream16"}
+
+
+def stats_rows(path):
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        rows[r["Name"]] = r
+    return rows
+
+
+def counter(dirpath, name):
+    """Per kernel name: mean per dispatch of counter `name` (KiB)."""
+    per = {}
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] == name:
+                per.setdefault(row.get("Kernel_Name", ""), []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    prof = os.path.join(ROOT, "profiles")
+    table = ["| config | dominant kernel | HIP-event avg (ms) | rocprof avg (ms) | rocprof calls | diff |",
+             "|---|---|---|---|---|---|"]
+    # ── per-config kernel stats + bench line ──
+    for d in sorted(glob.glob(os.path.join(src, "ks_*"))):
+        if not os.path.isdir(d):
+            continue
+        cfg = os.path.basename(d)[3:]
+        st = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+        full = os.path.join(d, "bench_full.json")
+        if not st or not os.path.exists(full):
+            print(f"{cfg}: incomplete", file=sys.stderr)
+            continue
+        shutil.copy(st[0], os.path.join(prof, f"{tag}_kernel_stats_{cfg}.csv"))
+        shutil.copy(full, os.path.join(prof, f"{tag}_bench_{cfg}.json"))
+        line = json.load(open(full))
+        r = line["roofline"]
+        kname = r["kernel"]
+        rows = stats_rows(st[0])
+        pats = DOMINANT.get(kname, [re.escape(kname)])
+        tot_ns, calls = 0.0, []
+        for p in pats:
+            hit = [(n, x) for n, x in rows.items() if re.search(p, n)]
+            for n, x in hit:
+                tot_ns += float(x["AverageNs"])
+                calls.append(int(x["Calls"]))
+        rp = tot_ns / 1e6
+        ev = r.get("avg_launch_ms") or 0.0
+        diff = (ev - rp) / rp if rp else float("nan")
+        table.append(f"| {cfg} | {kname} | {ev:.4f} | {rp:.4f} | {'/'.join(map(str, calls))} | {100 * diff:+.1f} % |")
+    # ── PMC calibration per access class ──
+    calib = {}
+    for k, nbytes in KNOWN.items():
+        f, _ = counter(os.path.join(src, f"calib_{k}_FETCH_SIZE"), "FETCH_SIZE")
+        w, _ = counter(os.path.join(src, f"calib_{k}_WRITE_SIZE"), "WRITE_SIZE")
+        fk = sum(v for n, v in f.items() if k in n)
+        wk = sum(v for n, v in w.items() if k in n)
+        if fk or wk:
+            calib[k] = {"known_bytes": nbytes, "fetch_kib": fk, "write_kib": wk,
+                        "bytes_per_fetch_kib": nbytes / (fk * 1024) if fk else None,
+                        "bytes_per_write_kib": nbytes / (wk * 1024) if wk else None}
+    if calib:
+        json.dump({"source": "scripts/micro/pmc_calib.cpp under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                             "(one counter per pass, kernel-include-regex per class)",
+                   "classes": calib}, open(os.path.join(prof, f"{tag}_pmc_calib.json"), "w"), indent=1)
+    # ── PMC traffic per config ──
+    for d in sorted(glob.glob(os.path.join(src, "pmc_*_FETCH_SIZE"))):
+        cfg = os.path.basename(d)[4:-len("_FETCH_SIZE")]
+        f, nf = counter(d, "FETCH_SIZE")
+        w, nw = counter(os.path.join(src, f"pmc_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
+        bj = os.path.join(src, f"pmc_{cfg}_FETCH_SIZE.json")
+        kname = json.load(open(bj))["roofline"]["kernel"] if os.path.exists(bj) else None
+        raw_f = sum(f.values()) * 1024
+        raw_w = sum(w.values()) * 1024
+        cls = FETCH_CLASS.get(kname, "dma16")
+        fac = (calib.get(cls) or {}).get("bytes_per_fetch_kib") or 2.0
+        rnd = (calib.get("rand16") or {}).get("bytes_per_fetch_kib")
+        res = {"kernel": kname, "config": cfg, "kernels": {k: {"fetch_kib": f.get(k), "write_kib": w.get(k),
+                                                                 "dispatches": [nf.get(k), nw.get(k)]}
+                                                             for k in sorted(set(f) | set(w))},
+               "fetch_bytes_raw": raw_f, "write_bytes": raw_w,
+               "fetch_class": cls, "fetch_factor": fac,
+               "fetch_bytes_per_launch": raw_f * fac,
+               "write_bytes_per_launch": raw_w,
+               "hbm_bytes_per_launch": raw_f * fac + raw_w,
+               "correction": f"FETCH_SIZE KiB x 1024 x {fac:.3f} ({cls}, profiles/{tag}_pmc_calib.json); "
+                             "WRITE_SIZE KiB x 1024"}
+        if rnd and cfg in ("c3s", "c3s_chain", "c4o", "c4o_chain"):
+            # the table tier's random 16-byte loads count at their own factor:
+            # the true bytes lie between the two corrections
+            res["fetch_bytes_if_all_random16"] = raw_f * rnd
+        json.dump(res, open(os.path.join(prof, f"{tag}_pmc_traffic_{cfg}.json"), "w"), indent=1)
+    open(os.path.join(prof, f"{tag}_rooflines.md"), "w").write(
+        f"# {tag}: dominant-kernel time, HIP events (bench.py) vs rocprofv3 --stats of the same run\n\n"
+        + "\n".join(table) + "\n")
+    print("\n".join(table))
+    if calib:
+        print(json.dumps(calib, indent=1))
+
+
+if __name__ == "__main__":
+    main()
