@@ -361,9 +361,14 @@ __device__ __forceinline__ uint64_t fold5(uint32_t lo, uint32_t hi, uint32_t tb)
 // crc_seg_rows with the five-bit tables (PB = 8: 13 tables; PB = 16: 26, the
 // second 13 for the piece's high 8 bytes, which do not wait for A).  SEG:
 // segment bytes (64 KiB for the encode passes, 16 KiB in the decode kernel).
-template <uint32_t PB, int kPf, uint32_t SEG = kCrcSegBytes>
+// kCopy (PB = 8): every piece wholly inside [start, copy_hi) is also stored
+// at its address + copy_delta (the decode kernel's in-place image of R, made
+// from the same loads as R's CRC).
+template <uint32_t PB, int kPf, uint32_t SEG = kCrcSegBytes, bool kCopy = false>
 __device__ __forceinline__ uint64_t crc_seg_rows5(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                  uint32_t tb, uint64_t klane) {
+                                                  uint32_t tb, uint64_t klane, intptr_t copy_delta = 0,
+                                                  uintptr_t copy_hi = 0) {
+	static_assert(!kCopy || PB == 8, "copy: 8-byte pieces");
 	static_assert(PB == 8 || PB == 16, "piece bytes");
 	constexpr uint32_t RB = 64 * PB, NR = SEG / RB;
 	static_assert(NR % kPf == 0, "rows per prefetch batch");
@@ -394,6 +399,14 @@ __device__ __forceinline__ uint64_t crc_seg_rows5(uintptr_t start, uint64_t len,
 			const int32_t o = (int32_t)((r0 + u) * RB);
 			xs[u] = piece_t{};
 			if (o + (int32_t)PB > z0) xs[u] = *reinterpret_cast<gpiece_t*>(p0 + (uintptr_t)(r0 + u) * RB);
+		}
+		if constexpr (kCopy) {
+#pragma unroll
+			for (int u = 0; u < kPf; ++u) {
+				const uintptr_t pa = p0 + (uintptr_t)(r0 + u) * RB;
+				if (pa >= start && pa + PB <= copy_hi)
+					*reinterpret_cast<__attribute__((address_space(1))) v2u*>(pa + copy_delta) = xs[u];
+			}
 		}
 #pragma unroll
 		for (int u = 0; u < kPf; ++u) {
@@ -1391,11 +1404,41 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
 	const uint64_t init = inplace ? (rl < bsz ? rl : bsz) : 0;
 	DPROF_T(tf0);
+	// R's CRC-64/XZ from the loads that make the in-place image (R is read
+	// once): 16 KiB segments as rows of 64 x 8 bytes, segment j on wave j % 4,
+	// each wave folding its segments Horner-wise; the image's whole 16-byte
+	// words are stored from the same pieces
+	const bool aligned_or = (((uintptr_t)O | (uintptr_t)R) & 15) == 0;
+	const bool rcrc_early = DG_CRC5 && a.crc_check && aligned_or && rl >= 8;
+	uint64_t racc = 0;
+	uint32_t rlast = ~0u;
+#if DG_CRC5
+	if (rcrc_early) {
+		const uint32_t t5 = (lds_addr(NX) + 255u) & ~255u;
+		uint64_t* T5 = reinterpret_cast<uint64_t*>(NX) + (t5 - lds_addr(NX)) / 8;
+		uint64_t* TK = T5 + 32 * kCrc5Tabs8;
+		const uint64_t* KF = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;
+		for (uint32_t k = tid; k < 32 * kCrc5Tabs8; k += kDecBlock) T5[k] = a.tables[kCrc5R8 + k];
+		for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
+		__syncthreads();
+		const uint64_t klane = a.tables[kCrcRowK8 + lane];
+		const uint32_t nseg = crc_nseg((uintptr_t)R, rl, kDecCrcSeg);
+		const uintptr_t copy_hi = (uintptr_t)R + init / 16 * 16;
+		for (uint32_t j = wave; j < nseg; j += kDecWaves) {
+			const uint64_t c = crc_seg_rows5<8, 4, kDecCrcSeg, true>((uintptr_t)R, rl, nseg, j, t5, klane,
+			                                                        (intptr_t)O - (intptr_t)R, copy_hi);
+			racc = (rlast != ~0u ? mul_nib(racc, TK) : 0ull) ^ c;
+			rlast = j;
+		}
+		__syncthreads();   // the tables' LDS is the parse's next
+	}
+#endif
 	{
 		uint64_t k0 = 0;
-		if ((((uintptr_t)O | (uintptr_t)R) & 15) == 0) {   // 16 B per thread, 4 in flight
+		if (aligned_or) {   // 16 B per thread, 4 in flight
 			const uint64_t n16 = init / 16;
-			for (uint64_t b = 0; b < n16; b += 4 * kDecBlock) {
+			const uint64_t ncopy = rcrc_early ? 0 : n16;   // (else made with R's CRC above)
+			for (uint64_t b = 0; b < ncopy; b += 4 * kDecBlock) {
 				typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 				u32x4 x[4];
 #pragma unroll
@@ -1699,7 +1742,10 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		for (int sp = 0; sp < 2; ++sp) {
 			uint64_t acc = 0;
 			uint32_t last = ~0u;
-			if (sl[sp] >= 8) {
+			if (sp == 0 && rcrc_early) {   // R's, from the fill
+				acc = racc;
+				last = rlast;
+			} else if (sl[sp] >= 8) {
 				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
 #if DG_CRC5
