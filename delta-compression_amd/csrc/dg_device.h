@@ -85,8 +85,11 @@ constexpr uint32_t kCrcRowK16 = kCrcRowsOff + 24 * 256, kCrcRowK8 = kCrcRowK16 +
 // (A ^ low 8 bytes), then 13 more with n = 1016 on the high 8 bytes
 constexpr uint32_t kCrc5Tabs8 = 13, kCrc5Tabs16 = 26;
 #ifndef DG_CRC5
-#define DG_CRC5 1   // the row passes use the five-bit tables (0: the byte tables)
+#define DG_CRC5 0   // 1: the encode's row passes use the five-bit tables (A/B; byte tables by default)
 #endif
+#ifndef DG_DEC_CRC
+#define DG_DEC_CRC 1   // decode kernel CRCs: 0 lane-contiguous segments at the end (R read twice),
+#endif                 // 1 byte-table rows with R's CRC from the in-place fill, 2 the same on five-bit tables
 constexpr uint32_t kCrc5R8 = kCrcRowK8 + 64, kCrc5R16 = kCrc5R8 + 32 * kCrc5Tabs8;
 constexpr uint32_t kCrcTabWords = kCrc5R16 + 32 * kCrc5Tabs16;
 

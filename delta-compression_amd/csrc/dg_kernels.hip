@@ -257,24 +257,28 @@ __global__ __launch_bounds__(kCrcWideBlock) void crc_segments_wide_kernel(CrcArg
 // tb + 2048 NC j + 8 NC b + 8 c; lane l reads copy l % NC (NC = 4: 8 lanes
 // of a 32-lane group per copy over 8 bank pairs instead of 32 lanes over 32);
 // tables j >= 8 from tbh = tb + 8 * 2048 NC (ds_read offsets are 16-bit).
-template <uint32_t PB, uint32_t NC, int kPf>
+// SEG: segment bytes; kCopy (PB = 8): pieces wholly inside [start, copy_hi)
+// are also stored at their address + copy_delta (as crc_seg_rows5).
+template <uint32_t PB, uint32_t NC, int kPf, uint32_t SEG = kCrcSegBytes, bool kCopy = false>
 __device__ __forceinline__ uint64_t crc_seg_rows(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                 uint32_t tb, uint32_t tbh, uint64_t klane) {
+                                                 uint32_t tb, uint32_t tbh, uint64_t klane,
+                                                 intptr_t copy_delta = 0, uintptr_t copy_hi = 0) {
 	static_assert(PB == 8 || PB == 16, "piece bytes");
-	constexpr uint32_t RB = 64 * PB, NR = kCrcSegBytes / RB;
+	static_assert(!kCopy || PB == 8, "copy: 8-byte pieces");
+	constexpr uint32_t RB = 64 * PB, NR = SEG / RB;
 	constexpr uint32_t TS = 2048 * NC, BS = 8 * NC;
 	static_assert(NR % kPf == 0, "rows per prefetch batch");
 	const uint32_t lane = lane_id();
 	const uintptr_t end = start + len;
 	const uintptr_t a0 = start & ~(uintptr_t)15;
 	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)nseg * kCrcSegBytes;   // may wrap below a0
-	const uintptr_t p0 = dom + (uintptr_t)j * kCrcSegBytes + (uintptr_t)lane * PB;
+	const uintptr_t dom = a1 - (uintptr_t)nseg * SEG;   // may wrap below a0
+	const uintptr_t p0 = dom + (uintptr_t)j * SEG + (uintptr_t)lane * PB;
 	// span edges relative to the lane's row-0 piece, clamped so the per-row
 	// tests stay in 32-bit arithmetic
 	auto clamp32 = [](intptr_t v) -> int32_t {
 		return (int32_t)(v < -(intptr_t)RB ? -(intptr_t)RB
-		                 : (v > (intptr_t)(kCrcSegBytes + RB) ? (intptr_t)(kCrcSegBytes + RB) : v));
+		                 : (v > (intptr_t)(SEG + RB) ? (intptr_t)(SEG + RB) : v));
 	};
 	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)p0);
 	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)p0);
@@ -301,6 +305,14 @@ __device__ __forceinline__ uint64_t crc_seg_rows(uintptr_t start, uint64_t len, 
 					xs[u].x = h.x;
 					xs[u].y = h.y;
 				}
+			}
+		}
+		if constexpr (kCopy) {
+#pragma unroll
+			for (int u = 0; u < kPf; ++u) {
+				const uintptr_t pa = p0 + (uintptr_t)(r0 + u) * RB;
+				if (pa >= start && pa + PB <= copy_hi)
+					*reinterpret_cast<__attribute__((address_space(1))) v2u*>(pa + copy_delta) = v2u{xs[u].x, xs[u].y};
 			}
 		}
 #pragma unroll
@@ -1328,6 +1340,37 @@ __device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uin
 	}
 }
 
+// The decode kernel's CRC segments (DG_DEC_CRC 1: byte-table rows, 2:
+// five-bit rows; 16 KiB segments as rows of 64 x 8 bytes).  The tables go to
+// LDS at tb (256-byte aligned, inside the dead doubling arrays), then the
+// nibble table of x^(8 * 64 KiB) (the Horner step of a wave's segments) at TK.
+struct DecCrc {
+	uint32_t tb;
+	const uint64_t* TK;
+	uint64_t klane;
+};
+__device__ __forceinline__ DecCrc dec_crc_tables(uint16_t* NX, const DecodeArgs& a) {
+	const uint32_t tid = threadIdx.x;
+	const uint32_t base = lds_addr(NX), tb = (base + 255u) & ~255u;
+	uint64_t* T = reinterpret_cast<uint64_t*>(NX) + (tb - base) / 8;
+	constexpr uint32_t nt = DG_DEC_CRC == 2 ? 32 * kCrc5Tabs8 : 8 * 256;
+	const uint32_t src = DG_DEC_CRC == 2 ? kCrc5R8 : kCrcRows8;
+	for (uint32_t k = tid; k < nt; k += kDecBlock) T[k] = a.tables[src + k];
+	uint64_t* TK = T + nt;
+	const uint64_t* KF = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;
+	for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
+	static_assert(8 * (8 * 256 + kCrcNibTabWords) + 256 <= 3 * kDecWin * 2, "CRC tables fit NX");
+	return DecCrc{tb, TK, a.tables[kCrcRowK8 + lane_id()]};
+}
+template <bool kCopy = false>
+__device__ __forceinline__ uint64_t dec_seg_crc(const DecCrc& t, uintptr_t start, uint64_t len, uint32_t nseg,
+                                                uint32_t j, intptr_t copy_delta = 0, uintptr_t copy_hi = 0) {
+	if constexpr (DG_DEC_CRC == 2)
+		return crc_seg_rows5<8, 4, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.klane, copy_delta, copy_hi);
+	else
+		return crc_seg_rows<8, 1, 8, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.tb, t.klane, copy_delta, copy_hi);
+}
+
 __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void decode_kernel(DecodeArgs a) {
 	const uint32_t i = blockIdx.x;
 	if (i >= a.n) return;
@@ -1409,25 +1452,18 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	// each wave folding its segments Horner-wise; the image's whole 16-byte
 	// words are stored from the same pieces
 	const bool aligned_or = (((uintptr_t)O | (uintptr_t)R) & 15) == 0;
-	const bool rcrc_early = DG_CRC5 && a.crc_check && aligned_or && rl >= 8;
+	const bool rcrc_early = DG_DEC_CRC != 0 && a.crc_check && aligned_or && rl >= 8;
 	uint64_t racc = 0;
 	uint32_t rlast = ~0u;
-#if DG_CRC5
+#if DG_DEC_CRC
 	if (rcrc_early) {
-		const uint32_t t5 = (lds_addr(NX) + 255u) & ~255u;
-		uint64_t* T5 = reinterpret_cast<uint64_t*>(NX) + (t5 - lds_addr(NX)) / 8;
-		uint64_t* TK = T5 + 32 * kCrc5Tabs8;
-		const uint64_t* KF = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;
-		for (uint32_t k = tid; k < 32 * kCrc5Tabs8; k += kDecBlock) T5[k] = a.tables[kCrc5R8 + k];
-		for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
+		const DecCrc ct = dec_crc_tables(NX, a);
 		__syncthreads();
-		const uint64_t klane = a.tables[kCrcRowK8 + lane];
 		const uint32_t nseg = crc_nseg((uintptr_t)R, rl, kDecCrcSeg);
 		const uintptr_t copy_hi = (uintptr_t)R + init / 16 * 16;
 		for (uint32_t j = wave; j < nseg; j += kDecWaves) {
-			const uint64_t c = crc_seg_rows5<8, 4, kDecCrcSeg, true>((uintptr_t)R, rl, nseg, j, t5, klane,
-			                                                        (intptr_t)O - (intptr_t)R, copy_hi);
-			racc = (rlast != ~0u ? mul_nib(racc, TK) : 0ull) ^ c;
+			const uint64_t c = dec_seg_crc<true>(ct, (uintptr_t)R, rl, nseg, j, (intptr_t)O - (intptr_t)R, copy_hi);
+			racc = (rlast != ~0u ? mul_nib(racc, ct.TK) : 0ull) ^ c;
 			rlast = j;
 		}
 		__syncthreads();   // the tables' LDS is the parse's next
@@ -1707,17 +1743,11 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		block_sync_global();   // every wave's output stores before any CRC read
 		const uint64_t* Lv = a.tables + 8 * 256;
 		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
-#if DG_CRC5
-		// LDS (the dead doubling arrays): the five-bit row tables (3.25 KiB,
-		// 256-byte aligned) and x^(8 * 64 KiB); 16 KiB segments read as rows
-		// of 64 x 8 bytes (coalesced), conflict-free lookups
-		const uint32_t t5 = (lds_addr(NX) + 255u) & ~255u;
-		uint64_t* T5 = reinterpret_cast<uint64_t*>(NX) + (t5 - lds_addr(NX)) / 8;
-		uint64_t* TK = T5 + 32 * kCrc5Tabs8;
-		static_assert(8 * (32 * kCrc5Tabs8 + kCrcNibTabWords) + 256 <= sizeof(NX), "CRC tables fit NX");
-		for (uint32_t k = tid; k < 32 * kCrc5Tabs8; k += kDecBlock) T5[k] = a.tables[kCrc5R8 + k];
-		for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
-		const uint64_t klane = a.tables[kCrcRowK8 + lane];
+#if DG_DEC_CRC
+		// LDS (the dead doubling arrays): the row tables and x^(8 * 64 KiB);
+		// 16 KiB segments read as rows of 64 x 8 bytes (coalesced)
+		const DecCrc ct = dec_crc_tables(NX, a);
+		const uint64_t* TK = ct.TK;
 #else
 		// LDS (the dead doubling arrays, 22 of 24 KiB): the slicing-by-4
 		// tables, the tree's levels x^(8 * 256 * 2^l) and x^(8 * 64 KiB)
@@ -1748,8 +1778,8 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			} else if (sl[sp] >= 8) {
 				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
-#if DG_CRC5
-					const uint64_t c = crc_seg_rows5<8, 4, kDecCrcSeg>(sa[sp], sl[sp], nseg, j, t5, klane);
+#if DG_DEC_CRC
+					const uint64_t c = dec_seg_crc(ct, sa[sp], sl[sp], nseg, j);
 #else
 					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, lds_addr(TS), TT);
 #endif

@@ -472,6 +472,49 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 	}
 	if (lane == 0) a.n_mem[J.chunk_base + c] = nm;
 
+	// The last member when no later run starts in the staged region (sparse
+	// edits: 1 MiB pairs at 1 %): its run has ended once 16 clean bytes follow
+	// its last mismatch inside the region, so x is known; its COPY runs to the
+	// first mismatch past the region (or the end E, the sentinel), found here
+	// from HBM, and that position is the next run start (>= 16 clean bytes
+	// before it) in a later chunk.  Without it the member stays unverified and
+	// the chain runs the exact epoch machinery from it.
+	uint32_t sn_last = 0;   // its next run start (offset from g0), 0: unknown
+	if (nm > 0 && nm == nrun && (int64_t)E > g0 + (int64_t)kStage) {
+		const uint32_t xl = L.last[kMaskWords - 1];   // last mismatch + 1 (the sentinel is past the region)
+		if (xl + 16 <= kStage) {
+			const uint8_t* V = a.ver + J.v_off;
+			const uint8_t* R = a.ref + J.r_off;
+			uint32_t y = ~0u;
+			for (uint64_t b = (uint64_t)(g0 + (int64_t)kStage); y == ~0u; b += 1024) {
+				if (b >= E) { y = E; break; }
+				const uint64_t p0 = b + 16ull * lane;
+				uint32_t m = 0;   // bit k: byte p0 + k differs (or is at/after E)
+				if (p0 < E) {
+					if (p0 + 16 <= E) {
+						uint4 v, r;
+						__builtin_memcpy(&v, V + p0, 16);
+						__builtin_memcpy(&r, R + p0, 16);
+						m = mismatch16(v, r);
+					} else {
+						for (uint32_t k = 0; k < 16; ++k)
+							if (p0 + k >= E || V[p0 + k] != R[p0 + k]) m |= 1u << k;
+					}
+				} else {
+					m = 0xFFFFu;
+				}
+				const uint64_t w = __ballot(m != 0u);
+				if (w) {
+					const uint32_t L0 = ffs64(w);
+					const uint32_t mb = rdlane(m, L0);
+					const uint64_t yy = b + 16ull * L0 + (uint32_t)__builtin_ctz(mb);
+					y = yy < E ? (uint32_t)yy : E;
+				}
+			}
+			sn_last = (uint32_t)((int64_t)y - g0);
+		}
+	}
+
 	const uint64_t q = J.q, qmag = J.q_magic;
 	const ModQ mq = make_modq(q, qmag);
 	VFilter<64> fs{L.filt};
@@ -487,13 +530,16 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 		const uint32_t i = k0 + lane;
 		const bool mine = i < k1;
 		const uint32_t s = mine ? L.run[i] : 0u;
-		const bool known = mine && i + 1 < nrun;
-		const uint32_t sn = known ? L.run[i + 1] : 0u;
+		const bool in_region = mine && i + 1 < nrun;   // the next run start is staged
+		const bool known = in_region || (mine && i + 1 == nrun && sn_last != 0u);
+		const uint32_t sn = in_region ? L.run[i + 1] : (known ? sn_last : 0u);
 		uint32_t x = 0;
-		if (known) {   // highest mismatch offset below sn, + 1
+		if (in_region) {   // highest mismatch offset below sn, + 1
 			const uint32_t j = sn >> 5, b = sn & 31u;
 			const uint32_t below = L.mask[j] & ((1u << b) - 1u);
 			x = below ? 32 * j + 32u - (uint32_t)__builtin_clz(below) : (j ? L.last[j - 1] : 0u);
+		} else if (known) {   // every staged mismatch is below sn
+			x = L.last[kMaskWords - 1];
 		}
 		const uint32_t T = x - s;
 		const bool shrt = known && T < 64;
@@ -593,8 +639,8 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			// (the first step's V window) and the COPY length
 			const uint64_t BA = __ballot(bad);
 			const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fb << 2), (int)w0);
+			const uint32_t snj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)sn);   // its next start
 			if (isT) {
-				const uint32_t snj = L.run[k0 + mj + 1];
 				const uint32_t xx = (uint32_t)(g0 + (int64_t)(ms_j + mt_j));
 				const uint32_t v = (BA & mem) == 0 ? 1u : 0u;
 				*(uint4*)(srec + 4 * mj) = make_uint4(xx, snj - (ms_j + mt_j), pw, v);

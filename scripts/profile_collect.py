@@ -133,6 +133,33 @@ def main():
             # the true bytes lie between the two corrections
             res["fetch_bytes_if_all_random16"] = raw_f * rnd
         json.dump(res, open(os.path.join(prof, f"{tag}_pmc_traffic_{cfg}.json"), "w"), indent=1)
+    # ── fresh-plan warm-up: per-dispatch durations of each config's dominant
+    #    kernel in launch order (the checked step, the profile pass, warmup, timed) ──
+    warm = {}
+    for d in sorted(glob.glob(os.path.join(src, "ks_*"))):
+        cfg = os.path.basename(d)[3:]
+        tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+        full = os.path.join(d, "bench_full.json")
+        if not tr or not os.path.exists(full):
+            continue
+        kname = json.load(open(full))["roofline"]["kernel"]
+        pats = DOMINANT.get(kname, [re.escape(kname)])
+        durs = []
+        for row in csv.DictReader(open(tr[0])):
+            if any(re.search(p, row["Kernel_Name"]) for p in pats[:1]):
+                durs.append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+        durs.sort()
+        ms = [x for _, x in durs]
+        if len(ms) >= 20:
+            k = len(ms)
+            warm[cfg] = {"dispatches": k, "first_10_ms": round(sum(ms[:10]) / 10, 4),
+                         "dispatch_10_to_40_ms": round(sum(ms[10:40]) / max(len(ms[10:40]), 1), 4),
+                         "last_20_ms": round(sum(ms[-20:]) / 20, 4),
+                         "per_dispatch_ms": [round(x, 4) for x in ms]}
+    if warm:
+        json.dump(warm, open(os.path.join(prof, f"{tag}_warmup.json"), "w"), indent=1)
+        for c, w in warm.items():
+            print(c, {k: v for k, v in w.items() if k != "per_dispatch_ms"})
     open(os.path.join(prof, f"{tag}_rooflines.md"), "w").write(
         f"# {tag}: dominant-kernel time, HIP events (bench.py) vs rocprofv3 --stats of the same run\n\n"
         + "\n".join(table) + "\n")

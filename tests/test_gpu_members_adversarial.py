@@ -60,3 +60,48 @@ def test_members_adversarial(dg, ctx_mode, orc, q):
     got = dg.encode_batch([(R, V) for _, R, V in pairs], "onepass", p=16, q=q, ctx=ctx_mode)
     for (name, R, V), d in zip(pairs, got):
         assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
+
+
+def _sparse_pairs(seed):
+    """Sparse edits placed around the end of a chunk's staged region
+    (dg_members.hip: chunk c stages positions [2048 c - 16, 2048 c + 2288)):
+    the chunk's last run then has no later run start staged, and its COPY
+    runs to a mismatch found past the region -- just past it, several chunks
+    later, at a stream end, or to an identical tail."""
+    rng = random.Random(seed)
+    out = []
+    for k in (0, 1, 2, 15, 16, 17, 100, 700, 3000, 9000):
+        L = 65536 + rng.randrange(2) * rng.randrange(1, 4096)
+        R = rng.randbytes(L)
+        V = bytearray(R)
+        c = rng.randrange(4, 20)
+        last = 2048 * c + rng.randrange(1900, 2048)        # the chunk's last mismatch
+        V[last] ^= 0x5A
+        if rng.random() < 0.5:
+            V[last - rng.randrange(2, 15)] ^= 0x33       # a run of two
+        nxt = 2048 * c + 2288 + k                         # first mismatch past the staged region
+        if nxt < L:
+            V[nxt] ^= 0xA5
+        out.append((f"sparse_{k}", R, bytes(V)))
+    R = rng.randbytes(70000)
+    V = bytearray(R)
+    V[2048 * 9 + 2000] ^= 1                                # then identical to the end
+    out.append(("identical_tail", R, bytes(V)))
+    V2 = bytearray(R[:2048 * 9 + 2040]) + bytes([R[2048 * 9 + 2040] ^ 1])   # V ends inside the look-ahead
+    out.append(("short_v", R, bytes(V2)))
+    # 1 MiB, 0.1 % edits: most chunks end on such a member
+    R = rng.randbytes(1 << 20)
+    V = bytearray(R)
+    for _ in range(1000):
+        V[rng.randrange(len(V))] ^= 1 + rng.randrange(255)
+    out.append(("mib_sparse", R, bytes(V)))
+    return out
+
+
+@pytest.mark.parametrize("q", [1, 97])
+def test_members_sparse_chunk_ends(dg, ctx_mode, orc, q):
+    pairs = _sparse_pairs(7 + q)
+    got = dg.encode_batch([(R, V) for _, R, V in pairs], "onepass", p=16, q=q, ctx=ctx_mode)
+    for (name, R, V), d in zip(pairs, got):
+        assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
+        assert dg.decode(R, d, ctx=ctx_mode) == V, name
