@@ -99,7 +99,8 @@ struct EncodeArgs {
 	const uint8_t* ver;
 	const PairDev* pairs;
 	const PairPlanDev* pplan;
-	uint32_t n_pairs;
+	uint32_t n_pairs;          // pairs [pair0, n_pairs) of the batch in this launch
+	uint32_t pair0;
 	uint32_t p;
 	const uint64_t* powc;      // p constants: 263^(p-1-k) mod (2^61-1)
 	uint32_t* rec;             // 3 x u32 per COPY record (v, r, len)
@@ -164,6 +165,10 @@ constexpr uint32_t kSegTail = 0xFFFFFFFFu;
 constexpr uint32_t kMemChunk = 2048;
 constexpr uint32_t kMemAhead = 240;    // staged: [chunk - 16, chunk + 2048 + 240) = 2304 B
 constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
+// member plans pipeline the batch in up to kMemGroupsMax groups of
+// consecutive pairs, one per kMemGroupChunks chunks (C3: 4 groups)
+constexpr uint32_t kMemGroupsMax = 4;
+constexpr uint32_t kMemGroupChunks = 65536;
 
 struct SpecArgs {
 	const uint8_t* ref;
@@ -171,6 +176,7 @@ struct SpecArgs {
 	const PairDev* pairs;
 	const PairPlanDev* pplan;
 	const uint2* chunks;       // per wave: (pair, chunk)
+	uint32_t job0;             // wave w of the launch takes job job0 + w
 	uint32_t* mem_s;           // per member slot: epoch start s_k
 	uint32_t* n_mem;           // per chunk: members starting in it
 	uint32_t* srec;            // per member slot: (x, COPY length, ADD head, verified)
@@ -185,6 +191,7 @@ struct MemSerArgs {
 	const PairDev* pairs;
 	const PairPlanDev* pplan;
 	const uint2* chunks;
+	uint32_t job0;             // the launch's jobs: [job0, job0 + n_jobs)
 	const uint32_t* cmap;
 	const uint32_t* seg;
 	const uint32_t* nseg;
@@ -281,7 +288,7 @@ hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint3
 hipError_t launch_correcting_clear(const EncodeArgs& a, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
                              hipEvent_t ev_built, hipEvent_t ev_fork);
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st, bool chained = false);
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);

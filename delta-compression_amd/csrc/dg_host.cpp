@@ -418,6 +418,14 @@ struct dg_encode_plan {
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	// member plans: the batch runs as n_groups groups of consecutive pairs;
+	// group g's scan and serialisation (stream ser) overlap the member kernel
+	// of group g + 1 (VALU-bound beside memory-bound)
+	uint32_t n_groups = 1;
+	std::vector<uint32_t> grp_pair, grp_chunk;   // n_groups + 1 boundaries each
+	hipStream_t ser = nullptr;
+	std::vector<hipEvent_t> ev_grp;              // group g's chains done
+	hipEvent_t ev_ser = nullptr;                 // the last group serialised
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
@@ -839,6 +847,28 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		if (!mbad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
 			mbad = 1;
+		// pipeline groups: consecutive pairs, about equal chunk counts; only
+		// for batches big enough that a group still fills the GPU
+		{
+			uint32_t G = std::min<uint32_t>(kMemGroupsMax, std::max<uint32_t>(1u, P->n_chunks / kMemGroupChunks));
+			const char* gg = ab_env("DG_MEM_GROUPS");
+			if (gg) G = std::max<uint32_t>(1u, std::min<uint32_t>(kMemGroupsMax, (uint32_t)strtoul(gg, nullptr, 0)));
+			G = std::min<uint32_t>(G, std::max<uint32_t>(n, 1u));
+			P->grp_pair.assign(1, 0u);
+			P->grp_chunk.assign(1, 0u);
+			for (uint32_t g = 1; g < G; ++g) {
+				const uint64_t want = (uint64_t)P->n_chunks * g / G;
+				uint32_t i = P->grp_pair.back();
+				while (i < n && P->pp[i].chunk_base < want) ++i;
+				if (i > P->grp_pair.back() && i < n) {
+					P->grp_pair.push_back(i);
+					P->grp_chunk.push_back(P->pp[i].chunk_base);
+				}
+			}
+			P->grp_pair.push_back(n);
+			P->grp_chunk.push_back(P->n_chunks);
+			P->n_groups = (uint32_t)P->grp_pair.size() - 1;
+		}
 		if (mbad && ctx->onepass_members != 1) {
 			// automatic mode: member mode is an optimisation, so a batch that
 			// fits with the plain chain still gets a plan
@@ -893,6 +923,17 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			return set_err(ctx, DG_ERR_HIP, "side stream creation failed: %s", hipGetErrorString(e));
 		}
 	}
+	if (P->members && P->n_groups > 1) {
+		e = hipStreamCreateWithFlags(&P->ser, hipStreamNonBlocking);
+		P->ev_grp.assign(P->n_groups, nullptr);
+		for (auto& ev : P->ev_grp)
+			if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice);
+		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_ser, hipEventDisableTiming | hipEventReleaseToDevice);
+		if (e != hipSuccess) {
+			dg_encode_plan_destroy(P);
+			return set_err(ctx, DG_ERR_HIP, "serialiser stream creation failed: %s", hipGetErrorString(e));
+		}
+	}
 	*out = P;
 	return DG_OK;
 }
@@ -927,15 +968,15 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 	return P ? P->d_nrec.as<uint32_t>() : nullptr;
 }
 
-constexpr int kTimingEvents = 8;
-constexpr uint32_t kTimingAll = 0xFFu;
+constexpr int kTimingEvents = 8 + 2 * (int)kMemGroupsMax;   // + around each group's member kernel
+constexpr uint32_t kTimingAll = (1u << kTimingEvents) - 1u;
 // the events a run records: all, or around the dominant kernel(s) only —
 // the member kernel (2, 6), the correcting build and scan (2, 7, 3), the
 // plain onepass kernel (2, 3); member plans also 3 (the chains after the
 // member kernel: the routed plain chain dominates on data off diagonal 0)
 static uint32_t timing_mask(const dg_encode_plan_t* P) {
 	if (P->timing_mode != DG_TIMING_DOMINANT) return kTimingAll;
-	if (P->members) return (1u << 2) | (1u << 6) | (1u << 3);   // member kernel, then the chains
+	if (P->members) return (1u << 2) | (1u << 6) | (1u << 3) | (0xFFFFu << 8);   // member kernel(s), then the chains
 	if (P->algo == DG_ALGO_CORRECTING) return (1u << 2) | (1u << 7) | (1u << 3);
 	return (1u << 2) | (1u << 3);
 }
@@ -990,7 +1031,16 @@ int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** name
 		if (hipEventSynchronize(e[last]) != hipSuccess) return 0;
 		for (int i = 0; i < ns; ++i) {
 			float t = 0;
-			hipEventElapsedTime(&t, e[pairs[sel[i]][0]], e[pairs[sel[i]][1]]);
+			if (sel[i] == 5 && P->members && P->n_groups > 1) {
+				// pipelined groups: the member kernels' own time, summed
+				for (uint32_t g = 0; g < P->n_groups; ++g) {
+					float tg = 0;
+					hipEventElapsedTime(&tg, e[8 + 2 * g], e[9 + 2 * g]);
+					t += tg;
+				}
+			} else {
+				hipEventElapsedTime(&t, e[pairs[sel[i]][0]], e[pairs[sel[i]][1]]);
+			}
 			acc[i] += t;
 		}
 	}
@@ -1006,6 +1056,26 @@ int dg_encode_plan_set_timing_mode(dg_encode_plan_t* P, int mode) {
 	if (!P || (mode != DG_TIMING_ALL && mode != DG_TIMING_DOMINANT)) return DG_ERR_INVALID_ARG;
 	P->timing_mode = mode;
 	return DG_OK;
+}
+
+static MemSerArgs mem_ser_args(const dg_encode_plan_t* P, const uint8_t* d_ver, uint8_t* d_out, uint64_t out_cap,
+                               const uint64_t* d_offsets, int32_t* d_status) {
+	MemSerArgs m{};
+	m.ver = d_ver;
+	m.pairs = P->d_pairs.as<PairDev>();
+	m.pplan = P->d_pplan.as<PairPlanDev>();
+	m.chunks = P->d_chunks.as<uint2>();
+	m.cmap = P->d_cmap.as<uint32_t>();
+	m.seg = P->d_seg.as<uint32_t>();
+	m.nseg = P->d_nseg.as<uint32_t>();
+	m.mem_s = P->d_mem_s.as<uint32_t>();
+	m.srec = P->d_srec.as<uint32_t>();
+	m.rec = P->d_rec.as<uint32_t>();
+	m.offsets = d_offsets;
+	m.out = d_out;
+	m.out_cap = out_cap;
+	m.status = d_status;
+	return m;
 }
 
 int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t* d_ver,
@@ -1108,8 +1178,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				m.srec = P->d_srec.as<uint32_t>();
 				m.csum = P->d_csum.as<uint32_t>();
 				m.cmap = P->d_cmap.as<uint32_t>();
-				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
-				HIPCHK(ctx, rec(6, st));
 				a.csum = m.csum;
 				a.cmap = m.cmap;
 				a.seg = P->d_seg.as<uint32_t>();
@@ -1118,8 +1186,39 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
+				if (P->n_groups == 1) {
+					HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
+					HIPCHK(ctx, rec(6, st));
+					HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
+				} else {
+					// group g: member kernel, chains (run stream); then its scan
+					// and serialisation on the serialiser stream, beside group
+					// g + 1's member kernel
+					MemSerArgs ms = mem_ser_args(P, d_ver, d_out, out_cap, d_offsets, d_status);
+					for (uint32_t g = 0; g < P->n_groups; ++g) {
+						const uint32_t c0 = P->grp_chunk[g], c1 = P->grp_chunk[g + 1];
+						const uint32_t p0 = P->grp_pair[g], p1 = P->grp_pair[g + 1];
+						m.job0 = c0;
+						HIPCHK(ctx, rec(8 + 2 * g, st));
+						HIPCHK(ctx, launch_members(m, c1 - c0, ctx->n_cu, st));
+						HIPCHK(ctx, rec(9 + 2 * g, st));
+						if (g + 1 == P->n_groups) HIPCHK(ctx, rec(6, st));
+						a.pair0 = p0;
+						a.n_pairs = p1;
+						HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
+						HIPCHK(ctx, hipEventRecord(P->ev_grp[g], st));
+						HIPCHK(ctx, hipStreamWaitEvent(P->ser, P->ev_grp[g], 0));
+						HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>() + p0, d_offsets + p0, p1 - p0, P->ser, g > 0));
+						ms.job0 = c0;
+						HIPCHK(ctx, launch_member_serialize(ms, c1 - c0, ctx->n_cu, P->ser));
+					}
+					HIPCHK(ctx, hipEventRecord(P->ev_ser, P->ser));
+					a.pair0 = 0;
+					a.n_pairs = P->n;
+				}
+			} else {
+				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			}
-			HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 		} else {
 			// fresh R indexes (~0 = empty slot), then build + scan
 			a.ctab = P->d_ctab.as<uint32_t>();
@@ -1175,6 +1274,15 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		HIPCHK(ctx, rec(5, st));
 		return DG_OK;
 	}
+	if (P->members && P->n_groups > 1) {
+		// every group already scanned and serialised on the serialiser stream
+		HIPCHK(ctx, rec(4, st));
+		HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_ser, 0));
+		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+		HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
+		HIPCHK(ctx, rec(5, st));
+		return DG_OK;
+	}
 	// 3. exclusive scan of sizes -> packed offsets
 	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
 	SerArgs s{};
@@ -1194,21 +1302,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	//    be running), then join and patch them in
 	HIPCHK(ctx, rec(4, st));
 	if (P->members) {   // the chains' segment lists, one wave per chunk
-		MemSerArgs m{};
-		m.ver = d_ver;
-		m.pairs = s.pairs;
-		m.pplan = s.pplan;
-		m.chunks = P->d_chunks.as<uint2>();
-		m.cmap = P->d_cmap.as<uint32_t>();
-		m.seg = P->d_seg.as<uint32_t>();
-		m.nseg = P->d_nseg.as<uint32_t>();
-		m.mem_s = P->d_mem_s.as<uint32_t>();
-		m.srec = P->d_srec.as<uint32_t>();
-		m.rec = s.rec;
-		m.offsets = d_offsets;
-		m.out = d_out;
-		m.out_cap = out_cap;
-		m.status = d_status;
+		const MemSerArgs m = mem_ser_args(P, d_ver, d_out, out_cap, d_offsets, d_status);
 		HIPCHK(ctx, launch_member_serialize(m, P->n_chunks, ctx->n_cu, st));
 	} else {
 		HIPCHK(ctx, launch_serialize_wave(s, st));
@@ -1226,9 +1320,14 @@ void dg_encode_plan_destroy(dg_encode_plan_t* P) {
 	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
+	if (P->ser) hipStreamSynchronize(P->ser);
 	if (P->ev_fork) hipEventDestroy(P->ev_fork);
 	if (P->ev_join) hipEventDestroy(P->ev_join);
+	for (auto& ev : P->ev_grp)
+		if (ev) hipEventDestroy(ev);
+	if (P->ev_ser) hipEventDestroy(P->ev_ser);
 	if (P->side) hipStreamDestroy(P->side);
+	if (P->ser) hipStreamDestroy(P->ser);
 	delete P;
 }
 

@@ -37,11 +37,14 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
 	return x;
 }
 
+// chained: off[0] already holds the offset this range starts at (the grand
+// total the previous range's scan wrote), else 0
 __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __restrict__ sz,
                                                           uint64_t* __restrict__ off,
-                                                          uint32_t n) {
+                                                          uint32_t n, uint32_t chained) {
 	__shared__ uint64_t wsum[16];
 	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+	const uint64_t base = chained ? off[0] : 0ull;
 	const uint32_t per = (n + 1023) / 1024;
 	const uint32_t b = tid * per, e = min(b + per, n);
 	uint64_t s = 0;
@@ -52,7 +55,7 @@ __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __rest
 	if (wave == 0) {
 		const uint64_t w = lane < 16 ? wsum[lane] : 0;
 		const uint64_t wi = wave_incl_scan64(w);
-		if (lane < 16) wsum[lane] = wi - w;   // exclusive wave offsets
+		if (lane < 16) wsum[lane] = base + wi - w;   // exclusive wave offsets
 	}
 	__syncthreads();
 	uint64_t run = wsum[wave] + incl - s;
@@ -778,8 +781,8 @@ hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_
 	return hipGetLastError();
 }
 
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
-	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st, bool chained) {
+	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n, chained ? 1u : 0u);
 	return hipGetLastError();
 }
 

@@ -700,7 +700,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_MEM_WAVES
 	__shared__ __attribute__((aligned(16))) ChunkLds L;
 	const uint32_t lane = lane_id();
 	JobCursor J;
-	J.start(a, blockIdx.x);
+	J.start(a, a.job0 + blockIdx.x);
 	{
 		const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
 		const uint8_t* V = a.ver + J.v_off;
@@ -837,8 +837,8 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 	__shared__ __attribute__((aligned(16))) uint8_t vbuf[kStage + 16];
 	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
 	const uint32_t lane = lane_id();
-	const uint32_t j0 = (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
-	const uint32_t j1 = (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
+	const uint32_t j0 = a.job0 + (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
+	const uint32_t j1 = a.job0 + (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
 	if (j0 >= j1) return;
 	SerFetch F, N;
 	F.J.start(a, j0);

@@ -1308,7 +1308,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
 	__shared__ __attribute__((aligned(4))) uint16_t lcache[kListCap];   // the diagonal batch's mismatch list; phase-C chunk bitmaps
-	const uint32_t pair = blockIdx.x;
+	const uint32_t pair = a.pair0 + blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
 	const PairPlanDev pp = a.pplan[pair];
@@ -1401,8 +1401,11 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 	if (a.n_pairs == 0) return hipSuccess;
 	if (p == 16 && aligned16 && !force_global_src()) {
 		if (a.srec) {   // member plan: the member chain, and the plain chain for routed pairs
-			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(a.n_pairs), dim3(64), 0, st, a);
-			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(a.n_pairs), dim3(64), 0, st, a);
+			// (pairs [pair0, n_pairs): one group of a pipelined run)
+			const uint32_t g = a.n_pairs - a.pair0;
+			if (g == 0) return hipSuccess;
+			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), 0, st, a);
+			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), 0, st, a);
 		} else {
 			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), 0, st, a);
 		}
