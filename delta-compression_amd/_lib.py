@@ -147,6 +147,8 @@ def _load() -> C.CDLL:
                                       C.POINTER(i32)]),
         "dg_encode_pipelined": (C.c_int, [vp, C.c_int, vp, vp, C.POINTER(Pair), u32, C.POINTER(DiffOptions), u64,
                                           vp, u64, C.POINTER(u64), C.POINTER(i32)]),
+        "dg_encode_pipelined_multi": (C.c_int, [C.POINTER(vp), u32, C.c_int, vp, vp, C.POINTER(Pair), u32,
+                                                C.POINTER(DiffOptions), u64, vp, u64, C.POINTER(u64), C.POINTER(i32)]),
         "dg_host_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
         "dg_host_free": (None, [vp]),
         "dg_crc64_xz": (C.c_int, [vp, u8p, sz, C.c_uint8 * 8]),
@@ -407,11 +409,13 @@ def encode_batch(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: i
 def encode_pipelined(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", p: int = SEED_LEN,
                      q: int = TABLE_SIZE, buf_cap: int = BUF_CAP, max_table: int = MAX_TABLE_SIZE,
                      chunk_bytes: int = 0, pinned: bool = False, align: int = 16, out_cap: Optional[int] = None,
-                     ctx: Optional[Context] = None) -> List[bytes]:
+                     ctx: Optional[Context] = None, ctxs: Optional[Sequence[Context]] = None) -> List[bytes]:
     """Many pairs host-to-host through dg_encode_pipelined (chunked, two chunks in
     flight).  The pairs are laid out in host arenas `align` bytes apart, pinned
-    (dg_host_alloc) or pageable (bytearray)."""
-    ctx = ctx or default_context()
+    (dg_host_alloc) or pageable (bytearray).  ctxs: one context per device,
+    through dg_encode_pipelined_multi (byte-balanced pair ranges, one host
+    thread per device, deltas packed in pair order)."""
+    ctx = ctx or (ctxs[0] if ctxs else default_context())
     n = len(pairs)
     if n == 0:
         return []
@@ -442,8 +446,13 @@ def encode_pipelined(pairs: Sequence[Tuple[bytes, bytes]], algorithm="onepass", 
         offs = (C.c_uint64 * (n + 1))()
         st = (C.c_int32 * n)()
         o = _opts(p, q, buf_cap, max_table)
-        ctx.check(lib.dg_encode_pipelined(ctx.handle, _algo(algorithm), hr, hv, pa, n, C.byref(o), chunk_bytes,
-                                          ho, cap, offs, st), "dg_encode_pipelined")
+        if ctxs:
+            hs = (C.c_void_p * len(ctxs))(*[c.handle for c in ctxs])
+            ctx.check(lib.dg_encode_pipelined_multi(hs, len(ctxs), _algo(algorithm), hr, hv, pa, n, C.byref(o),
+                                                    chunk_bytes, ho, cap, offs, st), "dg_encode_pipelined_multi")
+        else:
+            ctx.check(lib.dg_encode_pipelined(ctx.handle, _algo(algorithm), hr, hv, pa, n, C.byref(o), chunk_bytes,
+                                              ho, cap, offs, st), "dg_encode_pipelined")
         res = []
         for i in range(n):
             if st[i]:

@@ -165,10 +165,13 @@ constexpr uint32_t kSegTail = 0xFFFFFFFFu;
 constexpr uint32_t kMemChunk = 2048;
 constexpr uint32_t kMemAhead = 240;    // staged: [chunk - 16, chunk + 2048 + 240) = 2304 B
 constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
-// member plans pipeline the batch in up to kMemGroupsMax groups of
-// consecutive pairs, one per kMemGroupChunks chunks (C3: 4 groups)
+// member plans can pipeline the batch in up to kMemGroupsMax groups of
+// consecutive pairs (A/B: DG_MEM_GROUPS).  Off by default: measured C3 440 ->
+// 404 GiB/s and c3s 93 -> 64 (each group's chains become a launch of a
+// quarter of the pairs, and the serialiser's persistent waves hold the CUs
+// the next launches wait for; profiles/r04_experiments.md)
 constexpr uint32_t kMemGroupsMax = 4;
-constexpr uint32_t kMemGroupChunks = 65536;
+constexpr uint32_t kMemGroupsDefault = 1;
 
 struct SpecArgs {
 	const uint8_t* ref;

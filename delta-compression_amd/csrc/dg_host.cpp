@@ -850,7 +850,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		// pipeline groups: consecutive pairs, about equal chunk counts; only
 		// for batches big enough that a group still fills the GPU
 		{
-			uint32_t G = std::min<uint32_t>(kMemGroupsMax, std::max<uint32_t>(1u, P->n_chunks / kMemGroupChunks));
+			uint32_t G = kMemGroupsDefault;
 			const char* gg = ab_env("DG_MEM_GROUPS");
 			if (gg) G = std::max<uint32_t>(1u, std::min<uint32_t>(kMemGroupsMax, (uint32_t)strtoul(gg, nullptr, 0)));
 			G = std::min<uint32_t>(G, std::max<uint32_t>(n, 1u));

@@ -283,6 +283,109 @@ void dg_host_free(void* p) {
 	if (p) hipHostFree(p);
 }
 
+int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algorithm_t algo, const uint8_t* h_ref,
+                              const uint8_t* h_ver, const dg_pair_t* pairs, uint32_t n, const dg_diff_options_t* opts,
+                              uint64_t chunk_bytes, uint8_t* h_out, uint64_t out_cap, uint64_t* out_offsets,
+                              int32_t* status) {
+	if (!ctxs || n_ctx == 0 || !out_offsets || (n && (!pairs || !h_ref || !h_ver || !h_out))) return DG_ERR_INVALID_ARG;
+	for (uint32_t d = 0; d < n_ctx; ++d)
+		if (!ctxs[d]) return DG_ERR_INVALID_ARG;
+	if (n_ctx == 1 || n < 2)
+		return dg_encode_pipelined(ctxs[0], algo, h_ref, h_ver, pairs, n, opts, chunk_bytes, h_out, out_cap,
+		                           out_offsets, status);
+	dg_diff_options_t o;
+	if (opts) o = *opts; else dg_diff_options_default(&o);
+	const uint64_t p = o.p ? o.p : DG_SEED_LEN;
+	// contiguous ranges, balanced by input bytes (shard.py balanced_ranges)
+	uint64_t total = 0;
+	for (uint32_t i = 0; i < n; ++i) total += pairs[i].r_len + pairs[i].v_len;
+	const uint32_t D = std::min<uint32_t>(n_ctx, n);
+	std::vector<uint32_t> cut{0};
+	{
+		uint64_t acc = 0;
+		uint32_t i = 0;
+		for (uint32_t d = 1; d < D; ++d) {
+			const double target = (double)total * d / D;
+			while (i < n && (double)(acc + pairs[i].r_len + pairs[i].v_len) <= target) acc += pairs[i].r_len + pairs[i].v_len, ++i;
+			cut.push_back(i);
+		}
+		cut.push_back(n);
+	}
+	// each range into its own buffer (its output bound, as dg_encode_plan's)
+	struct Range {
+		uint32_t lo = 0, hi = 0;
+		std::vector<uint8_t> out;
+		std::vector<uint64_t> off;
+		std::vector<int32_t> st;
+		int rc = DG_OK;
+	};
+	std::vector<Range> R(D);
+	for (uint32_t d = 0; d < D; ++d) {
+		Range& r = R[d];
+		r.lo = cut[d];
+		r.hi = cut[d + 1];
+		uint64_t bound = 0;
+		for (uint32_t i = r.lo; i < r.hi; ++i) {
+			const uint64_t vl = pairs[i].v_len;
+			bound += algo == DG_ALGO_CORRECTING ? 57 + vl + 22 * (vl / p) : 35 + vl + (vl / p) * (p < 22 ? 22 - p : 0);
+		}
+		try {
+			r.out.resize(std::max<uint64_t>(bound, 1));
+			r.off.resize((size_t)(r.hi - r.lo) + 1);
+			r.st.resize(std::max<uint32_t>(r.hi - r.lo, 1));
+		} catch (...) {
+			return DG_ERR_NOMEM;
+		}
+	}
+	{
+		std::vector<std::thread> th;
+		for (uint32_t d = 0; d < D; ++d)
+			th.emplace_back([&, d] {
+				Range& r = R[d];
+				if (r.hi == r.lo) {
+					r.off[0] = 0;
+					return;
+				}
+				r.rc = dg_encode_pipelined(ctxs[d], algo, h_ref, h_ver, pairs + r.lo, r.hi - r.lo, opts, chunk_bytes,
+				                           r.out.data(), r.out.size(), r.off.data(), r.st.data());
+			});
+		for (auto& t : th) t.join();
+	}
+	// pack in pair order
+	uint64_t pos = 0;
+	int rc_all = DG_OK;
+	out_offsets[0] = 0;
+	for (uint32_t d = 0; d < D; ++d) {
+		Range& r = R[d];
+		const uint32_t m = r.hi - r.lo;
+		if (r.rc != DG_OK && r.rc != DG_ERR_CAPACITY) {   // the range failed as a whole
+			for (uint32_t k = 0; k < m; ++k) {
+				out_offsets[r.lo + k + 1] = pos;
+				if (status) status[r.lo + k] = r.rc;
+			}
+			if (rc_all == DG_OK) rc_all = r.rc;
+			continue;
+		}
+		const uint64_t bytes = r.off[m];
+		if (pos + bytes > out_cap) {   // h_out is full from here on
+			for (uint32_t k = 0; k < m; ++k) {
+				out_offsets[r.lo + k + 1] = pos;
+				if (status) status[r.lo + k] = r.st[k] != DG_OK ? r.st[k] : DG_ERR_CAPACITY;
+			}
+			rc_all = DG_ERR_CAPACITY;
+			continue;
+		}
+		par_memcpy(h_out + pos, r.out.data(), bytes);
+		for (uint32_t k = 0; k < m; ++k) {
+			out_offsets[r.lo + k + 1] = pos + r.off[k + 1];
+			if (status) status[r.lo + k] = r.st[k];
+			if (!status && r.st[k] != DG_OK && rc_all == DG_OK) rc_all = r.st[k];
+		}
+		pos += bytes;
+	}
+	return rc_all;
+}
+
 int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h_ref, const uint8_t* h_ver,
                         const dg_pair_t* pairs, uint32_t n, const dg_diff_options_t* opts,
                         uint64_t chunk_bytes, uint8_t* h_out, uint64_t out_cap, uint64_t* out_offsets,

@@ -271,6 +271,22 @@ int dg_encode_pipelined(dg_context_t *ctx, dg_algorithm_t algo,
                         uint8_t *h_out, uint64_t out_cap,
                         uint64_t *out_offsets, int32_t *status);
 
+/* The same host-to-host encode sharded over several devices (one context
+ * per device, e.g. the 8 MI355X of a node): contiguous pair
+ * ranges balanced by sum(|R|+|V|), one host thread per context running
+ * dg_encode_pipelined on its range into a private buffer (sized by the
+ * range's output bound), then the ranges' deltas are packed into h_out in
+ * pair order: h_out, out_offsets and status read exactly as the one-device
+ * call leaves them.  No bytes move between devices.  n_ctx == 1 is
+ * dg_encode_pipelined.  Returns as dg_encode_pipelined (the first failing
+ * range's code when status is NULL). */
+int dg_encode_pipelined_multi(dg_context_t *const *ctxs, uint32_t n_ctx, dg_algorithm_t algo,
+                              const uint8_t *h_ref, const uint8_t *h_ver,
+                              const dg_pair_t *pairs, uint32_t n_pairs,
+                              const dg_diff_options_t *opts, uint64_t chunk_bytes,
+                              uint8_t *h_out, uint64_t out_cap,
+                              uint64_t *out_offsets, int32_t *status);
+
 /* Pinned (page-locked) host memory for the arenas and outputs above. */
 int  dg_host_alloc(dg_context_t *ctx, uint64_t bytes, void **out);
 void dg_host_free(void *p);

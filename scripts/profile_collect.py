@@ -62,8 +62,9 @@ def main():
     tag = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", tag)
     prof = os.path.join(ROOT, "profiles")
-    table = ["| config | dominant kernel | HIP-event avg (ms) | rocprof avg (ms) | rocprof calls | diff |",
-             "|---|---|---|---|---|---|"]
+    table = ["| config | dominant kernel | HIP-event avg, timed steps (ms) | rocprof avg, all calls (ms) | rocprof calls | "
+             "rocprof trace, last K dispatches (ms) | diff (trace vs events) |",
+             "|---|---|---|---|---|---|---|"]
     # ── per-config kernel stats + bench line ──
     for d in sorted(glob.glob(os.path.join(src, "ks_*"))):
         if not os.path.isdir(d):
@@ -89,8 +90,21 @@ def main():
                 calls.append(int(x["Calls"]))
         rp = tot_ns / 1e6
         ev = r.get("avg_launch_ms") or 0.0
-        diff = (ev - rp) / rp if rp else float("nan")
-        table.append(f"| {cfg} | {kname} | {ev:.4f} | {rp:.4f} | {'/'.join(map(str, calls))} | {100 * diff:+.1f} % |")
+        # the timed steps are the last K dispatches of each dominant kernel
+        k_steps = int(line.get("steps") or 0)
+        tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+        last = float("nan")
+        if tr and k_steps:
+            per = {}
+            for row in csv.DictReader(open(tr[0])):
+                for p in pats:
+                    if re.search(p, row["Kernel_Name"]):
+                        per.setdefault(p, []).append((int(row["Start_Timestamp"]),
+                                                      (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
+            last = sum(sum(x for _, x in sorted(v)[-k_steps:]) / k_steps for v in per.values()) if per else float("nan")
+        diff = (last - ev) / ev if ev else float("nan")
+        table.append(f"| {cfg} | {kname} | {ev:.4f} | {rp:.4f} | {'/'.join(map(str, calls))} | {last:.4f} | "
+                     f"{100 * diff:+.1f} % |")
     # ── PMC calibration per access class ──
     calib = {}
     for k, nbytes in KNOWN.items():
@@ -117,7 +131,13 @@ def main():
         raw_w = sum(w.values()) * 1024
         cls = FETCH_CLASS.get(kname, "dma16")
         fac = (calib.get(cls) or {}).get("bytes_per_fetch_kib") or 2.0
-        rnd = (calib.get("rand16") or {}).get("bytes_per_fetch_kib")
+        # the table tier's random 16-byte loads: pmc_calib shows FETCH_SIZE
+        # tallies 64 B per such load (4x its useful bytes); whether the line
+        # moved is 64 or 128 B the counter cannot tell, so these configs carry
+        # both readings: x1 (64-B requests) and x2 (as the streaming reads)
+        table_tier = cfg in ("c3s", "c3s_chain", "c4o", "c4o_chain")
+        if table_tier:
+            cls, fac = "mixed: LDS-DMA windows + random 16-byte table loads", 1.0
         res = {"kernel": kname, "config": cfg, "kernels": {k: {"fetch_kib": f.get(k), "write_kib": w.get(k),
                                                                  "dispatches": [nf.get(k), nw.get(k)]}
                                                              for k in sorted(set(f) | set(w))},
@@ -128,10 +148,11 @@ def main():
                "hbm_bytes_per_launch": raw_f * fac + raw_w,
                "correction": f"FETCH_SIZE KiB x 1024 x {fac:.3f} ({cls}, profiles/{tag}_pmc_calib.json); "
                              "WRITE_SIZE KiB x 1024"}
-        if rnd and cfg in ("c3s", "c3s_chain", "c4o", "c4o_chain"):
-            # the table tier's random 16-byte loads count at their own factor:
-            # the true bytes lie between the two corrections
-            res["fetch_bytes_if_all_random16"] = raw_f * rnd
+        if table_tier:
+            res["hbm_bytes_upper"] = raw_f * 2.0 + raw_w
+            res["correction"] = ("FETCH_SIZE KiB x 1024 x 1 (lower reading: every request 64 B as tallied); "
+                                 "hbm_bytes_upper: x 2 (every request 128 B tallied at 64 B, as streaming reads); "
+                                 "WRITE_SIZE KiB x 1024")
         json.dump(res, open(os.path.join(prof, f"{tag}_pmc_traffic_{cfg}.json"), "w"), indent=1)
     # ── fresh-plan warm-up: per-dispatch durations of each config's dominant
     #    kernel in launch order (the checked step, the profile pass, warmup, timed) ──

@@ -93,3 +93,29 @@ def test_pipelined_limits_invalidate_cached_plans(dg, orc):
         ctx.set_limit(dg.LIMIT_ONEPASS_MEMBERS, mode)
         assert dg.encode_pipelined(pairs, "onepass", q=97, pinned=True, ctx=ctx) == want
     ctx.close()
+
+
+@pytest.mark.parametrize("n_dev", [2, 3])
+@pytest.mark.parametrize("algo", ["onepass", "correcting"])
+def test_pipelined_multi_device(dg, orc, n_dev, algo):
+    """dg_encode_pipelined_multi: pair ranges balanced by bytes over several
+    contexts (the one-GPU box: contexts on device 0, each with its own
+    streams, plans and staging, driven by its own host thread), deltas packed
+    in pair order exactly as the one-device call packs them."""
+    pairs = _pairs(40 + n_dev, 70)
+    ctxs = [dg.Context(0) for _ in range(n_dev)]
+    try:
+        got = dg.encode_pipelined(pairs, algo, p=16, q=97, chunk_bytes=96 << 10, pinned=True, ctxs=ctxs)
+        one = dg.encode_pipelined(pairs, algo, p=16, q=97, chunk_bytes=96 << 10, pinned=True, ctx=ctxs[0])
+        assert got == one
+        a = ONEPASS if algo == "onepass" else CORRECTING
+        for i, ((R, V), d) in enumerate(zip(pairs, got)):
+            assert d == orc.encode(a, R, V, p=16, q=97), i
+        # a tight h_out: the ranges that fit are packed, the rest report DG_ERR_CAPACITY
+        total = sum(len(d) for d in got)
+        with pytest.raises(dg.DeltaError) as e:
+            dg.encode_pipelined(pairs, algo, p=16, q=97, pinned=True, ctxs=ctxs, out_cap=total // 2)
+        assert e.value.code == 7
+    finally:
+        for c in ctxs:
+            c.close()
