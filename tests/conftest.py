@@ -70,10 +70,13 @@ def torch_cuda():
     return torch
 
 
-@pytest.fixture(scope="session", params=["members", "chain"])
+@pytest.fixture(scope="session", params=["members", "chain", "auto"])
 def ctx_mode(dg, request):
     """A context per onepass chain mode (DG_LIMIT_ONEPASS_MEMBERS): verified
-    diagonal members first, or the plain per-pair chain."""
+    diagonal members first, the plain per-pair chain, or the automatic choice
+    (members for large pairs; pairs whose matches leave diagonal 0 routed to
+    the segment chains, dg_onepass.hip)."""
     c = dg.Context(0)
-    c.set_limit(dg.LIMIT_ONEPASS_MEMBERS, dg.MEMBERS_ON if request.param == "members" else dg.MEMBERS_OFF)
+    c.set_limit(dg.LIMIT_ONEPASS_MEMBERS, {"members": dg.MEMBERS_ON, "chain": dg.MEMBERS_OFF,
+                                           "auto": dg.MEMBERS_AUTO}[request.param])
     return c
