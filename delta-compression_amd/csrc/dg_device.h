@@ -49,9 +49,6 @@ struct PairPlanDev {
 	// correcting, CRC of R in the build: x^(-8 pad), pad = |R| rounded up to
 	// 32 KiB minus |R| (the build's zero padding)
 	uint64_t crc_unpad;
-	// onepass segment chains (routed pairs of member plans): the pair's
-	// segment jobs [seg_job0, seg_job0 + seg_n), 0 = none
-	uint32_t seg_job0, seg_n;
 };
 
 struct CrcSegDev {        // one wave's CRC segment
@@ -147,21 +144,6 @@ struct EncodeArgs {
 	// automatic member mode: pairs averaging fewer verified members per chunk
 	// than this run the plain chain (its records as one segment); 0 = never
 	uint32_t route_min;
-	// per pair, written by the member chain: 0 member pair, 1 routed (to the
-	// segment chains when seg_jobs is set), 2 routed to the plain chain
-	uint32_t* route_flag;
-	// segment chains (dg_onepass.hip, onepass16_seg_kernel + segment_stitch_kernel):
-	// per job (pair, v start, r start, v stop); records kRecWordsOnepass words,
-	// seg_rec_cap per job; per job record count and status
-	const uint4* seg_jobs;
-	uint32_t n_seg_jobs;
-	uint32_t seg_rec_cap;
-	uint32_t* seg_rec;
-	uint32_t* seg_nrec;
-	int32_t* seg_st;
-	// per pair, from the stitch when the chains did not meet: the plain chain
-	// resumes at (v0, r0) after nrec records (already in place) and dsz bytes
-	uint4* seg_resume;
 	// --verbose diagnostics (correcting; nullptr = off): per pair 8 u64 —
 	// build seeds passing the checkpoint, slots stored, scan checkpoints, fp
 	// mismatches, byte mismatches, matches, k, passing seeds whose slot is in
@@ -175,17 +157,6 @@ struct EncodeArgs {
 };
 
 constexpr uint32_t kSegTail = 0xFFFFFFFFu;
-
-// Segment chains: a routed pair of at least 2 kSegBytes runs as one chain per
-// kSegBytes of V, chain k from a guessed state at k kSegBytes to kSegOverlap
-// past the next start; chains are spliced where two of them start the same
-// epoch (dg_onepass.hip)
-constexpr uint32_t kSegBytes = 32768;
-constexpr uint32_t kSegOverlap = 4096;
-// a segment chain gives up when an epoch runs this far past its stop (the
-// pair's chains cannot meet there; the plain chain resumes instead)
-constexpr uint32_t kSegAbort = 16384;
-constexpr int32_t kSegAborted = 100;   // seg_st of such a chain
 
 // Speculative diagonal members of the onepass chain (dg_members.hip): one
 // wave per chunk of kMemChunk positions, with kMemAhead bytes of look-ahead

@@ -421,9 +421,6 @@ struct dg_encode_plan {
 	// member plans: the batch runs as n_groups groups of consecutive pairs;
 	// group g's scan and serialisation (stream ser) overlap the member kernel
 	// of group g + 1 (VALU-bound beside memory-bound)
-	// routed pairs of member plans: segment chains (dg_onepass.hip)
-	uint32_t n_seg_jobs = 0, seg_rec_cap = 0;
-	DevBuf d_seg_jobs, d_seg_rec, d_seg_nrec, d_seg_st, d_route_flag, d_seg_resume;
 	uint32_t n_groups = 1;
 	std::vector<uint32_t> grp_pair, grp_chunk;   // n_groups + 1 boundaries each
 	hipStream_t ser = nullptr;
@@ -872,47 +869,6 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			P->grp_chunk.push_back(P->n_chunks);
 			P->n_groups = (uint32_t)P->grp_pair.size() - 1;
 		}
-		// segment chains for the pairs the automatic mode routes to the plain
-		// chain (decided on the device; every pair of >= 2 pieces gets jobs)
-		const char* sgs = ab_env("DG_SEGMENTS");
-		if (P->route_min && P->n_groups == 1 && o.p == 16 && !(sgs && sgs[0] == '0')) {
-			std::vector<uint32_t> sj;
-			for (uint32_t i = 0; i < n; ++i) {
-				const uint64_t vl = pairs[i].v_len, rl = pairs[i].r_len;
-				P->pp[i].seg_job0 = (uint32_t)(sj.size() / 4);
-				P->pp[i].seg_n = 0;
-				if (std::min(vl, rl) < 2ull * kSegBytes) continue;
-				const uint32_t K = (uint32_t)((vl + kSegBytes - 1) / kSegBytes);
-				for (uint32_t k = 0; k < K; ++k) {
-					const uint64_t vs = (uint64_t)k * kSegBytes;
-					const uint64_t rs = k ? std::min<uint64_t>(vs * rl / vl, rl) : 0;
-					const uint64_t stop = k + 1 < K ? vs + kSegBytes + kSegOverlap : 0xFFFFFFFFull;
-					sj.insert(sj.end(), {i, (uint32_t)vs, (uint32_t)rs, (uint32_t)stop});
-				}
-				P->pp[i].seg_n = K;
-			}
-			P->n_seg_jobs = (uint32_t)(sj.size() / 4);
-			P->seg_rec_cap = (kSegBytes + kSegOverlap + 4096) / 16 + 4;
-			if (P->n_seg_jobs) {
-				int sbad = 0;
-				sbad |= P->d_seg_jobs.alloc(4ull * sj.size());
-				sbad |= P->d_seg_rec.alloc(16ull * P->seg_rec_cap * P->n_seg_jobs);
-				sbad |= P->d_seg_nrec.alloc(4ull * P->n_seg_jobs);
-				sbad |= P->d_seg_st.alloc(4ull * P->n_seg_jobs);
-				sbad |= P->d_route_flag.alloc(4ull * std::max<uint32_t>(n, 1));
-				sbad |= P->d_seg_resume.alloc(16ull * std::max<uint32_t>(n, 1));
-				if (!sbad && hipMemcpy(P->d_seg_jobs.p, sj.data(), 4 * sj.size(), hipMemcpyHostToDevice) != hipSuccess)
-					sbad = 1;
-				if (sbad) {   // an optimisation: without the memory, the plain chain
-					(void)hipGetLastError();
-					for (DevBuf* b : {&P->d_seg_jobs, &P->d_seg_rec, &P->d_seg_nrec, &P->d_seg_st, &P->d_route_flag,
-				                  &P->d_seg_resume})
-						b->release();
-					P->n_seg_jobs = 0;
-					for (uint32_t i = 0; i < n; ++i) P->pp[i].seg_n = 0;
-				}
-			}
-		}
 		if (mbad && ctx->onepass_members != 1) {
 			// automatic mode: member mode is an optimisation, so a batch that
 			// fits with the plain chain still gets a plan
@@ -1230,16 +1186,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
-				if (P->n_seg_jobs) {
-					a.route_flag = P->d_route_flag.as<uint32_t>();
-					a.seg_jobs = P->d_seg_jobs.as<uint4>();
-					a.n_seg_jobs = P->n_seg_jobs;
-					a.seg_rec_cap = P->seg_rec_cap;
-					a.seg_rec = P->d_seg_rec.as<uint32_t>();
-					a.seg_nrec = P->d_seg_nrec.as<uint32_t>();
-					a.seg_st = P->d_seg_st.as<int32_t>();
-					a.seg_resume = P->d_seg_resume.as<uint4>();
-				}
 				if (P->n_groups == 1) {
 					HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 					HIPCHK(ctx, rec(6, st));

@@ -698,20 +698,16 @@ struct PairResult {
 	int32_t st;
 };
 
-// kSeg: one segment chain (job `job`): the epochs from the job's guessed
-// state until an epoch starts at or past its stop, records to the job's own
-// area; the trailing ADD and the pair's outputs are the stitch's.
-template <bool kMembers, class Src, bool kRouted = false, bool kSeg = false>
+template <bool kMembers, class Src, bool kRouted = false>
 __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a, uint32_t pair,
                                              const PairDev& pd, const PairPlanDev& pp, uint32_t p,
-                                             uint32_t* bm, uint32_t* cscr, uint32_t job = 0) {
+                                             uint32_t* bm, uint32_t* cscr) {
 	const uint32_t lane = lane_id();
 	const uint32_t vl = uni((uint32_t)pd.v_len), rl = uni((uint32_t)pd.r_len);
 	const uint64_t q = uni64(pp.q), qmag = uni64(pp.q_magic);
 	const ModQ mq = make_modq(q, qmag);
-	const uint32_t rec_cap = kSeg ? a.seg_rec_cap : uni(pp.rec_cap);
-	uint32_t* __restrict__ rec = kSeg ? a.seg_rec + (uint64_t)kRecWordsOnepass * a.seg_rec_cap * job
-	                                  : a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base;
+	const uint32_t rec_cap = uni(pp.rec_cap);
+	uint32_t* __restrict__ rec = a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base;
 
 	uint32_t nrec = 0;
 	uint64_t dsz = 26;   // header (25) + END
@@ -731,25 +727,9 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		tslot = -1;
 	};
 
-	uint32_t v0 = 0, r0 = 0, v_stop = 0xFFFFFFFFu;
-	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
-	if constexpr (kSeg) {
-		const uint4 jb = a.seg_jobs[job];
-		v0 = uni(jb.y);
-		r0 = uni(jb.z);
-		v_stop = uni(jb.w);
-	}
-	if constexpr (kRouted) {
-		if (a.seg_jobs) {   // after segment chains that did not meet: resume where the stitch stopped
-			const uint4 rs = a.seg_resume[pair];
-			v0 = uni(rs.x);
-			r0 = uni(rs.y);
-			nrec = uni(rs.z);
-			dsz = uni(rs.w);
-			at_mismatch = nrec > 0;
-		}
-	}
+	uint32_t v0 = 0, r0 = 0;
 	bool scanning = vl > 0;
+	bool at_mismatch = false;   // (v0, r0) is where the last extension stopped
 	bool skipA = false;         // the epoch is known to be long: phase B from step 0
 	// Backoff of the diagonal batch and of phase A: either only pays when most
 	// epochs resolve there (substitutions); after k failures in a row the next
@@ -880,7 +860,6 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 	while (scanning) {
 		skipA = false;
-		if (kSeg && v0 >= v_stop) break;   // the next chain's region and the overlap are covered
 		if (members && mem_live && v0 == r0 && v0 > s_cur) {
 			[[maybe_unused]] const uint64_t tr0 = PROF_NOW();
 			if constexpr (Src::kPhaseA) PROF_ADD(src, P_RESYNCS, 1);
@@ -1020,11 +999,6 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 		for (uint32_t c = 0; !matched; ++c) {
 			const uint32_t b0 = 64 * c;
 			if (b0 >= nlive) { scanning = false; break; }   // both streams exhausted
-			if (kSeg && v_stop != 0xFFFFFFFFu && (uint64_t)v0 + b0 >= (uint64_t)v_stop + kSegAbort) {
-				st = kSegAborted;
-				scanning = false;
-				break;
-			}
 			const uint32_t step = b0 + lane;
 			const bool cv = step < nv, cr = step < nr;
 			[[maybe_unused]] const uint64_t tb1 = PROF_NOW();
@@ -1307,13 +1281,6 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	if ((members || routed) && (dsz >> 32)) st = 7;   // segment offsets are 32-bit
 
 	if (tslot >= 0) release_table();
-	if constexpr (kSeg) {
-		if (lane == 0) {
-			a.seg_nrec[job] = nrec;
-			a.seg_st[job] = st;
-		}
-		return PairResult{nrec, dsz, st};
-	}
 	if (lane == 0) {
 		a.n_rec[pair] = nrec;
 		a.dsize[pair] = dsz;
@@ -1355,13 +1322,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 			uint32_t v = 0;
 			for (uint32_t c = lane_id(); c < nch; c += 64) v += a.csum[2ull * (pp.chunk_base + c)];
 			const bool member_pair = rdlane(wave_incl_scan(v), 63) >= a.route_min * nch;
-			// (the member chain, launched first, records the decision for the
-			// segment chains; a routed pair they cover takes the plain chain
-			// only when their stitch failed)
-			if (kMembers && a.route_flag && lane_id() == 0)
-				a.route_flag[pair] = member_pair ? 0u : (a.seg_jobs && pp.seg_n ? 1u : 2u);
 			if (member_pair != kMembers) return;
-			if (kRouted && a.seg_jobs && uni(a.route_flag[pair]) != 2u) return;
 		}
 	}
 	WinSrc src;
@@ -1415,165 +1376,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #endif
 }
 
-// ── segment chains (routed pairs of member plans: matches off diagonal 0) ──
-//
-// A pair's epochs form one serial chain (onepass.c:32-297), but an epoch's
-// outcome depends only on its start (v0, r0): every match flushes both tables
-// (:263).  So the pair is cut into kSegBytes pieces of V and chain k starts an
-// epoch at a guessed state (k kSegBytes, r proportional) -- chain 0 at (0, 0),
-// the true start -- and runs until an epoch starts kSegOverlap past the next
-// piece.  Once the true chain starts an epoch where chain k + 1 also started
-// one, the rest of it IS chain k + 1's.  On data whose matches follow the
-// edits (insertions, deletions, moved blocks) two chains that find a match in
-// the same clean stretch end it at the same mismatch, so they meet within a
-// few epochs of the guess.  segment_stitch_kernel finds the first common epoch
-// start of consecutive chains and concatenates their records; a pair whose
-// chains do not meet within the overlap runs the plain chain instead
-// (route_flag 2), so the output is always the reference's.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER_EU, 8))) void onepass16_seg_kernel(EncodeArgs a) {
-	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
-	__shared__ uint32_t bm[256];
-	__shared__ __attribute__((aligned(4))) uint16_t lcache[kListCap];
-	const uint32_t job = blockIdx.x;
-	if (job >= a.n_seg_jobs) return;
-	const uint32_t pair = uni(a.seg_jobs[job].x);
-	if (uni(a.route_flag[pair]) != 1u) return;   // a member pair (or a plain-chain one)
-	const PairDev pd = a.pairs[pair];
-	const PairPlanDev pp = a.pplan[pair];
-	WinSrc src;
-	src.S[0] = a.ver + pd.v_off;
-	src.S[1] = a.ref + pd.r_off;
-	src.len[0] = (uint32_t)pd.v_len;
-	src.len[1] = (uint32_t)pd.r_len;
-	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
-	src.win = (lds_u8*)win;
-	src.lc = lcache;
-	src.powc = a.powc;
-	PROF_INIT(src)
-	onepass_pair<false, WinSrc, false, true>(src, a, pair, pd, pp, 16u, bm, (uint32_t*)lcache, job);
-	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
-}
-
-// One wave per pair: splice the pair's segment chains.  Epoch starts of chain
-// k: its start, then the end of each of its records (strictly increasing in
-// v and in r).  For each boundary the first epoch start of chain k at or past
-// chain k + 1's start that chain k + 1 also has (a binary search per lane over
-// chain k + 1's record ends) is the splice; the records before it come from
-// chain k, the rest from chain k + 1.
-__global__ __launch_bounds__(64) void segment_stitch_kernel(EncodeArgs a) {
-	const uint32_t pair = blockIdx.x;
-	if (pair >= a.n_pairs) return;
-	const uint32_t rf = uni(a.route_flag[pair]);
-	if (rf == 0u) return;   // a member pair
-	const uint32_t lane = lane_id();
-	if (rf == 2u) {         // no segment chains: the plain chain from the start
-		if (lane == 0) a.seg_resume[pair] = make_uint4(0u, 0u, 0u, 26u);
-		return;
-	}
-	const PairDev pd = a.pairs[pair];
-	const PairPlanDev pp = a.pplan[pair];
-	const uint32_t vl = (uint32_t)pd.v_len;
-	const uint32_t K = uni(pp.seg_n), j0 = uni(pp.seg_job0);
-	const uint32_t cap = a.seg_rec_cap;
-	uint32_t* __restrict__ out = a.rec + (uint64_t)kRecWordsOnepass * pp.rec_base;
-	const uint32_t rec_cap = uni(pp.rec_cap);
-	auto recs = [&](uint32_t k) { return a.seg_rec + (uint64_t)kRecWordsOnepass * cap * (j0 + k); };
-	// epoch start i of chain k (i <= its record count)
-	auto start_of = [&](uint32_t k, uint32_t i) -> uint2 {
-		if (i == 0) {
-			const uint4 jb = a.seg_jobs[j0 + k];
-			return make_uint2(jb.y, jb.z);
-		}
-		const uint4 r4 = *(const uint4*)(recs(k) + kRecWordsOnepass * (i - 1));
-		return make_uint2(r4.x + r4.z, r4.y + r4.z);
-	};
-	bool resume = false;           // the chains did not meet: the plain chain goes on from (ev, er)
-	uint32_t nout = 0, from = 0;   // records taken; chain k's first record to take
-	uint32_t ev = 0, er = 0;       // the current epoch start
-	uint64_t dsz = 26;
-	int32_t st = 0;
-	for (uint32_t k = 0; k < K; ++k) {
-		const uint32_t nk = uni((uint32_t)a.seg_nrec[j0 + k]);
-		const bool ok = a.seg_st[j0 + k] == 0;   // else valid up to its last record
-		uint32_t upto = nk, next_from = 0;       // take [from, upto) of chain k
-		bool found = false;
-		if (k + 1 < K && ok) {
-			const uint32_t n1 = uni((uint32_t)a.seg_nrec[j0 + k + 1]);
-			const uint32_t vs1 = uni(a.seg_jobs[j0 + k + 1].y);
-			for (uint32_t b = from; b <= nk && !found; b += 64) {
-				const uint32_t i = b + lane;
-				bool hit = false;
-				uint32_t at = 0;
-				if (i <= nk) {
-					const uint2 e = start_of(k, i);
-					if (e.x >= vs1) {
-						// chain k + 1's epoch starts are strictly increasing in v
-						uint32_t lo = 0, hi = n1 + 1;
-						while (hi - lo > 1) {
-							const uint32_t mid = (lo + hi) >> 1;
-							if (start_of(k + 1, mid).x <= e.x) lo = mid;
-							else hi = mid;
-						}
-						const uint2 f = start_of(k + 1, lo);
-						hit = f.x == e.x && f.y == e.y;
-						at = lo;
-					}
-				}
-				const uint64_t m = __ballot(hit);
-				if (m) {
-					const uint32_t L = ffs64(m);
-					upto = b + L;
-					next_from = rdlane(at, L);
-					found = true;
-				}
-			}
-		}
-		resume = !found && (k + 1 < K || !ok);
-		// copy records [from, upto) of chain k, the delta bytes they add
-		const uint32_t* src = recs(k);
-		for (uint32_t b = from; b < upto; b += 64) {
-			const uint32_t i = b + lane;
-			const bool live = i < upto;
-			uint4 r4 = make_uint4(0u, 0u, 0u, 0u);
-			uint32_t es = 0;
-			if (live) {
-				r4 = *(const uint4*)(src + kRecWordsOnepass * i);
-				es = start_of(k, i).x;   // this record's epoch start
-			}
-			if (live && nout + (i - from) < rec_cap) *(uint4*)(out + kRecWordsOnepass * (nout + (i - from))) = r4;
-			const uint32_t sz = live ? 13u + (r4.x > es ? 9u + (r4.x - es) : 0u) : 0u;
-			dsz += rdlane(wave_incl_scan(sz), 63);
-		}
-		if (upto > from) nout += upto - from;
-		const uint2 e = start_of(k, upto);   // the epoch start after the records taken
-		ev = e.x;
-		er = e.y;
-		if (nout > rec_cap) { st = 7; break; }
-		if (resume) break;
-		from = next_from;
-	}
-	if (st == 0 && (dsz >> 32)) st = 7;
-	if (st == 0 && resume) {
-		if (lane == 0) {
-			a.seg_resume[pair] = make_uint4(ev, er, nout, (uint32_t)dsz);
-			a.route_flag[pair] = 2u;   // the plain chain goes on from here
-		}
-		return;
-	}
-	if (ev < vl) dsz += 9ull + (vl - ev);   // trailing ADD (:268-275)
-	if (st == 0 && (dsz >> 32)) st = 7;
-	if (lane == 0) {
-		uint4* sg = (uint4*)(a.seg + 4ull * ((uint64_t)pp.chunk_base + 2ull * pair));
-		uint32_t ns = 0;
-		if (nout) sg[ns++] = make_uint4(0u, nout, 25u, 0u);
-		sg[ns++] = make_uint4(kSegTail, 0u, (uint32_t)(dsz - 1), ev);
-		a.nseg[pair] = ns;
-		a.n_rec[pair] = nout;
-		a.dsize[pair] = dsz;
-		a.status[pair] = st;
-	}
-}
-
 // any seed length or alignment, bytes from HBM/L2
 template <int PF>
 __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
@@ -1603,10 +1405,6 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 			const uint32_t g = a.n_pairs - a.pair0;
 			if (g == 0) return hipSuccess;
 			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), 0, st, a);
-			if (a.route_min && a.seg_jobs && a.n_seg_jobs && a.pair0 == 0) {
-				hipLaunchKernelGGL(onepass16_seg_kernel, dim3(a.n_seg_jobs), dim3(64), 0, st, a);
-				hipLaunchKernelGGL(segment_stitch_kernel, dim3(a.n_pairs), dim3(64), 0, st, a);
-			}
 			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), 0, st, a);
 		} else {
 			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), 0, st, a);

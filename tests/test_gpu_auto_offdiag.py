@@ -1,13 +1,12 @@
-"""Segment chains (dg_onepass.hip: onepass16_seg_kernel + segment_stitch_kernel).
+"""The automatic chain mode on large pairs whose matches leave diagonal 0.
 
-In the automatic mode, large pairs whose matches leave diagonal 0 run as one
-speculative chain per 32 KiB of V, chain k from a guessed state, spliced
-where two chains start the same epoch; a pair whose chains do not meet
-resumes the plain chain from the last valid epoch start.  Every delta here is
-compared with the oracle: pairs that meet quickly (shifts), pairs that never
-meet (unrelated streams: the plain chain from the start), pairs that meet
-for a while and then not (random stretches), long epochs across the piece
-boundaries (moved blocks, large insertions), lengths around the piece size.
+A member plan (mean pair >= 128 KiB) routes a pair whose chunks verify fewer
+than 2 diagonal members each to the plain chain (dg_onepass.hip,
+onepass16_kernel<false, true>), inside the same plan as the member pairs.
+Every delta is compared with the oracle: dense and sparse insertions and
+deletions, unrelated streams, a random stretch inside a shifted pair, moved
+blocks, a large insertion, V much shorter or longer than R, lengths around
+the member chunk size.
 """
 import random
 
@@ -66,7 +65,7 @@ def _pairs(seed):
 
 
 @pytest.mark.parametrize("q", [1, 97])
-def test_segment_chains_vs_oracle(dg, orc, q):
+def test_auto_mode_offdiagonal_vs_oracle(dg, orc, q):
     ctx = dg.Context(0)   # automatic mode
     try:
         pairs = _pairs(1234 + q)
