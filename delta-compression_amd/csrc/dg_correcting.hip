@@ -65,6 +65,36 @@ __device__ __forceinline__ uint64_t roll61(uint64_t fp, uint64_t nb, uint32_t in
 	return r >= kMersenne ? r - kMersenne : r;
 }
 
+// The same step on a weakly reduced fingerprint (any value <= M + 2 with
+// the high dword <= 2^29, i.e. the residue plus 0..2 M), for the build's
+// unrolled seed loop.  With fp = h 2^32 + l:
+//   P = l 263 + nb (one 32x32+64 multiply-add, nb straight from the table),
+//   Q = h 263 < 2^39, and Q 2^32 == (Q & (2^29-1)) 2^32 + (Q >> 29),
+//   t = P + (Q >> 29) + in + (Q & (2^29-1)) 2^32 < 2^62 + 2^42,
+// folded once: (t & M) + (t >> 61) <= M + 2.  The canonical value (the
+// checkpoint test needs it, not the next roll) is fp61_canon's.
+__device__ __forceinline__ uint64_t roll61w(uint64_t fp, uint64_t nb, uint32_t in) {
+	const uint64_t P = (uint64_t)(uint32_t)fp * (uint32_t)kBase + nb;
+	const uint64_t Q = (uint64_t)(uint32_t)(fp >> 32) * (uint32_t)kBase;
+	const uint32_t s = (uint32_t)(Q >> 29) + in;
+	// dword arithmetic with explicit carries (no 64-bit adds of zero-extended
+	// halves, which cost a register move each)
+	const uint32_t tl = (uint32_t)P + s;
+	const uint32_t th = (uint32_t)(P >> 32) + ((uint32_t)Q & 0x1FFFFFFFu) + (tl < s ? 1u : 0u);
+	const uint32_t f = th >> 29;
+	const uint32_t rl = tl + f;
+	const uint32_t rh = (th & 0x1FFFFFFFu) + (rl < f ? 1u : 0u);
+	return ((uint64_t)rh << 32) | rl;
+}
+
+// r <= M + 2 to [0, M): r - M = r + 1 - 2^61 leaves only the low dword + 1
+__device__ __forceinline__ uint64_t fp61_canon(uint64_t r) {
+	const bool ge = r >= kMersenne;
+	const uint32_t lo = (uint32_t)r + (ge ? 1u : 0u);
+	const uint32_t hi = ge ? 0u : (uint32_t)(r >> 32);
+	return ((uint64_t)hi << 32) | lo;
+}
+
 // x * c mod M for x < 2^61 and c < 2^32
 __device__ __forceinline__ uint64_t mulsmall61(uint64_t x, uint32_t c) {
 	return fold61c((x & 0xFFFFFFFFull) * c, (x >> 32) * c);
@@ -133,94 +163,113 @@ __device__ __forceinline__ uint32_t first_diff16(const uint32_t (&x)[4], bool ba
 	return bad;
 }
 
-// number of equal leading bytes of a[0..) and b[0..), at most lim
-__device__ uint32_t ext_fwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
+// Extensions (correcting.c:293-303) in steps of 4 KiB per wave: lane l holds
+// bytes [ml + 1024 u + 16 l, +16) of step u (BACK: back-offsets, i.e. the
+// bytes a[-(base+16)] .. a[-(base+1)]).  A step's loads are issued apart from
+// its compare, so the forward and the backward extension of one match share
+// their first round trip.
+template <int N>
+struct ExtStep {
+	uint32_t wa[N][4], wb[N][4];
+};
+
+template <bool BACK, int N>
+__device__ __forceinline__ void ext_load(const uint8_t* a, const uint8_t* b, uint32_t ml, uint32_t lim, ExtStep<N>& s) {
 	const uint32_t lane = lane_id();
-	uint32_t ml = 0;
+#pragma unroll
+	for (int u = 0; u < N; ++u) {
+		const uint32_t base = ml + 1024u * u + 16 * lane;
+		if (base + 16 <= lim) {
+			__builtin_memcpy(s.wa[u], BACK ? a - base - 16 : a + base, 16);   // one unaligned 16-byte load
+			__builtin_memcpy(s.wb[u], BACK ? b - base - 16 : b + base, 16);
+		}
+	}
+}
+
+// the step's compare: true with *len the extension's length when it ends in
+// this step (a mismatch, or lim)
+template <bool BACK, int N>
+__device__ __forceinline__ bool ext_eval(const uint8_t* a, const uint8_t* b, uint32_t ml, uint32_t lim,
+                                         const ExtStep<N>& s, uint32_t* len) {
+	const uint32_t lane = lane_id();
+	uint32_t bad[N];
+#pragma unroll
+	for (int u = 0; u < N; ++u) {
+		const uint32_t base = ml + 1024u * u + 16 * lane;
+		bad[u] = 16;
+		if (base + 16 <= lim) {
+			const uint32_t x[4] = {s.wa[u][0] ^ s.wb[u][0], s.wa[u][1] ^ s.wb[u][1], s.wa[u][2] ^ s.wb[u][2],
+			                       s.wa[u][3] ^ s.wb[u][3]};
+			bad[u] = first_diff16(x, BACK);
+		} else if (base < lim) {   // the last bytes before lim: no read beyond them
+			const uint32_t n = lim - base;
+			uint32_t e = n;
+			for (uint32_t t = 0; t < n; ++t) {
+				const bool ne = BACK ? *(a - (base + t + 1)) != *(b - (base + t + 1)) : a[base + t] != b[base + t];
+				if (e == n && ne) e = t;
+			}
+			bad[u] = e;   // == n when all equal: a mismatch at lim
+		}
+	}
+#pragma unroll
+	for (int u = 0; u < N; ++u) {
+		const uint64_t m = __ballot(bad[u] < 16);
+		if (m) {
+			const uint32_t f = ffs64(m);
+			*len = umin_(lim, ml + 1024u * u + 16 * f + rdlane(bad[u], f));
+			return true;
+		}
+	}
+	if (ml + 1024u * N >= lim) {
+		*len = lim;
+		return true;
+	}
+	return false;
+}
+
+// the rest of an extension from ml on
+template <bool BACK>
+__device__ uint32_t ext_from(const uint8_t* a, const uint8_t* b, uint32_t ml, uint32_t lim) {
+	uint32_t len = lim;
 	while (ml < lim) {
-		uint32_t wa[kExtChunks][4], wb[kExtChunks][4];
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint32_t base = ml + 1024u * u + 16 * lane;
-			if (base + 16 <= lim) {
-				ld16u(a + base, wa[u]);
-				ld16u(b + base, wb[u]);
-			}
-		}
-		uint32_t bad[kExtChunks];
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint32_t base = ml + 1024u * u + 16 * lane;
-			bad[u] = 16;
-			if (base + 16 <= lim) {
-				const uint32_t x[4] = {wa[u][0] ^ wb[u][0], wa[u][1] ^ wb[u][1], wa[u][2] ^ wb[u][2], wa[u][3] ^ wb[u][3]};
-				bad[u] = first_diff16(x, false);
-			} else if (base < lim) {   // the last bytes before lim: no read beyond them
-				const uint32_t n = lim - base;
-				uint32_t e = n;
-				for (uint32_t t = 0; t < n; ++t)
-					if (e == n && a[base + t] != b[base + t]) e = t;
-				bad[u] = e;   // == n when all equal: a mismatch at lim
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint64_t m = __ballot(bad[u] < 16);
-			if (m) {
-				const uint32_t f = ffs64(m);
-				return umin_(lim, ml + 1024u * u + 16 * f + rdlane(bad[u], f));
-			}
-		}
+		ExtStep<kExtChunks> s;
+		ext_load<BACK>(a, b, ml, lim, s);
+		if (ext_eval<BACK>(a, b, ml, lim, s, &len)) return len;
 		ml += 1024u * kExtChunks;
 	}
 	return lim;
 }
 
-// number of equal bytes going backwards: a[-1] == b[-1], a[-2] == b[-2], ...,
-// at most lim
-__device__ uint32_t ext_bwd(const uint8_t* a, const uint8_t* b, uint32_t lim) {
-	const uint32_t lane = lane_id();
-	uint32_t ml = 0;
-	while (ml < lim) {
-		// lane covers back-offsets [base, base + 16): bytes a[-(base+16)] .. a[-(base+1)]
-		uint32_t wa[kExtChunks][4], wb[kExtChunks][4];
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint32_t base = ml + 1024u * u + 16 * lane;
-			if (base + 16 <= lim) {
-				ld16u(a - base - 16, wa[u]);
-				ld16u(b - base - 16, wb[u]);
-			}
-		}
-		uint32_t bad[kExtChunks];
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint32_t base = ml + 1024u * u + 16 * lane;
-			bad[u] = 16;
-			if (base + 16 <= lim) {
-				const uint32_t x[4] = {wa[u][0] ^ wb[u][0], wa[u][1] ^ wb[u][1], wa[u][2] ^ wb[u][2], wa[u][3] ^ wb[u][3]};
-				bad[u] = first_diff16(x, true);
-			} else if (base < lim) {   // the last bytes before lim: no read beyond them
-				const uint32_t n = lim - base;
-				uint32_t e = n;
-				for (uint32_t t = 0; t < n; ++t) {
-					const uint32_t d = base + t + 1;
-					if (e == n && *(a - d) != *(b - d)) e = t;
-				}
-				bad[u] = e;
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < kExtChunks; ++u) {
-			const uint64_t m = __ballot(bad[u] < 16);
-			if (m) {
-				const uint32_t f = ffs64(m);
-				return umin_(lim, ml + 1024u * u + 16 * f + rdlane(bad[u], f));
-			}
-		}
-		ml += 1024u * kExtChunks;
-	}
-	return lim;
+// both extensions of a seed match: forward a[0..) vs b[0..) up to flim,
+// backward a[-1], a[-2], ... vs b[-1], ... up to blim; their first steps
+// (2 KiB each) together.  The first steps stay at the register footprint of
+// one 4 KiB step: the V CRC rows kernel runs beside this one and needs room.
+constexpr int kFwdFirst = 1, kBwdFirst = 1;
+struct ExtPair {
+	ExtStep<kFwdFirst> f;
+	ExtStep<kBwdFirst> b;
+};
+
+__device__ __forceinline__ void ext_pair_load(const uint8_t* fa, const uint8_t* fb, uint32_t flim, const uint8_t* ba,
+                                             const uint8_t* bb, uint32_t blim, ExtPair& e) {
+	ext_load<false>(fa, fb, 0, flim, e.f);
+	ext_load<true>(ba, bb, 0, blim, e.b);
+}
+
+__device__ __forceinline__ void ext_pair_eval(const uint8_t* fa, const uint8_t* fb, uint32_t flim, const uint8_t* ba,
+                                             const uint8_t* bb, uint32_t blim, const ExtPair& e, uint32_t* fwd,
+                                             uint32_t* bwd) {
+	if (blim == 0) *bwd = 0;
+	else if (!ext_eval<true>(ba, bb, 0, blim, e.b, bwd)) *bwd = ext_from<true>(ba, bb, 1024u * kBwdFirst, blim);
+	if (flim == 0) *fwd = 0;
+	else if (!ext_eval<false>(fa, fb, 0, flim, e.f, fwd)) *fwd = ext_from<false>(fa, fb, 1024u * kFwdFirst, flim);
+}
+
+__device__ __forceinline__ void ext_both(const uint8_t* fa, const uint8_t* fb, uint32_t flim, const uint8_t* ba,
+                                        const uint8_t* bb, uint32_t blim, uint32_t* fwd, uint32_t* bwd) {
+	ExtPair e;
+	ext_pair_load(fa, fb, flim, ba, bb, blim, e);
+	ext_pair_eval(fa, fb, flim, ba, bb, blim, e, fwd, bwd);
 }
 
 }  // namespace
@@ -390,7 +439,8 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 				if constexpr (kMode == 0) {
 					const uint32_t f = mod_q_small(fp, ck.mf);
 					slot = f >> ck.mshift;
-					pass = (f & ((1u << ck.mshift) - 1u)) == ck.k && slot < ck.cap;
+					// (slot < cap always: m = ceil(|F| / cap), dg_host.cpp:629)
+					pass = (f & ((1u << ck.mshift) - 1u)) == ck.k;
 				} else if constexpr (kMode == 1) {
 					pass = ckpt_test(fp, ck, &slot);
 				} else {
@@ -402,32 +452,52 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 			// fold), covering every byte of R; the build only the seeds
 			const uint64_t lim = crc_wide ? rl : (build ? seeds : 0);
 			const uint64_t iters = (lim + kCrcStride - 1) / kCrcStride;
-			for (uint64_t it = 0; it < iters; ++it) {
+			// a lane's full 32-seed piece (p = 16) is held in registers as
+			// R[s0 .. s0+47), the 48th byte only if it exists; the next
+			// iteration's piece is loaded before this one is hashed, so with
+			// one 1024-thread block per CU the load latency is not exposed
+			auto full_piece = [&](uint64_t s0) {
+				return p == 16 && build && s0 < seeds && seeds - s0 >= kBuildSeedsPerLane;
+			};
+			auto fetch = [&](uint64_t s0, uint32_t (&w)[12]) {   // branch-free, so nothing waits on it
+				__builtin_memcpy(w, R + s0, 32);
+				// bytes 32..47; at the end of R (s0 + 47 == |R|) bytes 31..46,
+				// shifted down by the iteration that uses the piece
+				__builtin_memcpy(w + 8, R + s0 + (s0 + 48 <= rl ? 32 : 31), 16);
+			};
+			// one iteration over buffer `w` (already fetched when held), the
+			// next iteration's piece prefetched into `nx`; the loop alternates
+			// the two buffers, so no register copy waits on the loads
+			auto step = [&](uint64_t it, uint32_t (&w)[12], uint32_t (&nx)[12]) -> bool {
 				const uint64_t s0 = (uint64_t)tid * kBuildSeedsPerLane + it * kCrcStride;
-				if (!CRC && s0 >= seeds) break;
+				if (!CRC && s0 >= seeds) return false;
 				const uint32_t cnt = build && s0 < seeds
 				                         ? (uint32_t)(seeds - s0 < kBuildSeedsPerLane ? seeds - s0 : kBuildSeedsPerLane)
 				                         : 0u;
-				uint32_t w[12];   // R[s0 .. s0+47), the 48th byte only if it exists
-				bool held = false;
-				if (p == 16 && cnt == kBuildSeedsPerLane) {
-					__builtin_memcpy(w, R + s0, 32);
-					if (s0 + 48 <= rl) {
-						__builtin_memcpy(w + 8, R + s0 + 32, 16);
-					} else {
-						__builtin_memcpy(w + 8, R + s0 + 32, 12);
-						w[11] = (uint32_t)R[s0 + 44] | ((uint32_t)R[s0 + 45] << 8) | ((uint32_t)R[s0 + 46] << 16);
+				const bool held = full_piece(s0);
+				if (it + 1 < iters && full_piece(s0 + kCrcStride)) fetch(s0 + kCrcStride, nx);
+				if (held) {
+					if (s0 + 48 > rl) {
+						w[8] = __builtin_amdgcn_alignbit(w[9], w[8], 8);
+						w[9] = __builtin_amdgcn_alignbit(w[10], w[9], 8);
+						w[10] = __builtin_amdgcn_alignbit(w[11], w[10], 8);
+						w[11] >>= 8;
 					}
-					held = true;
 					auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
 					// two independent rolling chains (seeds 0..15 and 16..31)
 					uint64_t fa = fp16_dot(w[0], w[1], w[2], w[3]);
 					uint64_t fb = fp16_dot(w[4], w[5], w[6], w[7]);
 #pragma unroll
 					for (uint32_t j = 0; j < kBuildSeedsPerLane / 2; ++j) {
-						if (j) {   // roll (hash.c:62-98)
-							fa = roll61(fa, nb[byte_at(j - 1)], byte_at(j + 15));
-							fb = roll61(fb, nb[byte_at(j + 15)], byte_at(j + 31));
+						if (j) {   // roll (hash.c:62-98), weakly reduced
+							fa = roll61w(fa, nb[byte_at(j - 1)], byte_at(j + 15));
+							fb = roll61w(fb, nb[byte_at(j + 15)], byte_at(j + 31));
+						}
+						// a weakly reduced value >= M is ~2^-60 likely: one
+						// compare per seed, the subtract only in a wave that has one
+						if (__ballot(fa >= kMersenne || fb >= kMersenne)) {
+							fa = fp61_canon(fa);
+							fb = fp61_canon(fb);
 						}
 						insert(fa, (uint32_t)(s0 + j));
 						insert(fb, (uint32_t)(s0 + 16 + j));
@@ -456,6 +526,13 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 					for (uint32_t j = 0; j < 8; ++j) c = slice4(c, w[j], CT);
 					acc = (it ? mul_nib(acc, CT + 4 * 256) : 0ull) ^ c;
 				}
+				return true;
+			};
+			uint32_t ba[12], bb[12];
+			if (iters && full_piece((uint64_t)tid * kBuildSeedsPerLane)) fetch((uint64_t)tid * kBuildSeedsPerLane, ba);
+			for (uint64_t it = 0; it < iters; it += 2) {
+				if (!step(it, ba, bb)) break;
+				if (it + 1 < iters && !step(it + 1, bb, ba)) break;
 			}
 		};
 		if (ck.mf.ok && ck.mshift >= 0) run(std::integral_constant<int, 0>{});
@@ -498,7 +575,7 @@ struct RingEnt {
 	uint32_t vs, ve, r_off, kind;   // kind: 1 COPY, 2 ADD
 };
 
-__global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(64, 4) void correcting_scan_kernel(EncodeArgs a) {
 	extern __shared__ RingEnt ring[];   // buf_cap + 1 entries
 	const uint32_t pair = blockIdx.x;
 	const uint32_t lane = lane_id();
@@ -553,11 +630,12 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 		while (st == 0 && vc + p <= vl) {
 			// ── positions vc .. vc+63: fingerprint, checkpoint, lookup, memcmp ──
 			const uint32_t pos = vc + lane;
+			const bool in_v = pos + p <= vl;
 			bool hit = false, passed = false, fpm = false, bm = false;
 			uint32_t off = kNone;
-			if (pos + p <= vl) {
-				uint32_t wv[4];
-				uint64_t fp;
+			uint32_t wv[4] = {0, 0, 0, 0};
+			uint64_t fp = 0;
+			if (in_v) {
 				if (p == 16) {   // dot-product fingerprint of the 16 bytes (dg_devutil.h)
 					ld16u(V + pos, wv);
 					fp = fp16_dot(wv[0], wv[1], wv[2], wv[3]);
@@ -568,24 +646,37 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 				if (ck.mf.ok ? ckpt_test(fp, ck, &slot) : checkpoint_slot(fp, pp, k, &slot)) {
 					passed = true;
 					off = H[slot];
-					if (off != kNone) {   // correcting.c:268-285: verify the seed bytes
-						if (p == 16) {
-							uint32_t wr[4];
-							ld16u(R + off, wr);
-							hit = ((wr[0] ^ wv[0]) | (wr[1] ^ wv[1]) | (wr[2] ^ wv[2]) | (wr[3] ^ wv[3])) == 0u;
-						} else {
-							hit = true;
-							for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
-						}
-						if (a.stats && !hit) {   // the reference's stored-fingerprint test (:254-283)
-							const bool fpeq = window_fp<0>(R + off, p, a.powc) == fp;
-							fpm = !fpeq;
-							bm = fpeq;
-						}
-					}
 				} else if (a.stats) {   // a checkpoint whose f / m is past the table (:242, :268)
 					uint64_t sl;
 					passed = checkpoint_only(fp, pp, k, &sl);
+				}
+			}
+			const uint64_t C = __ballot(off != kNone);   // candidates, in position order
+			// The first candidate is usually the match: its extensions' first
+			// steps are loaded together with every candidate's seed bytes, so a
+			// verified first candidate costs no round trip of its own.
+			ExtPair ex;
+			uint32_t vc0 = 0, ro0 = 0;
+			if (C) {
+				const uint32_t j0 = ffs64(C);
+				vc0 = uni(vc + j0);
+				ro0 = uni(rdlane(off, j0));
+				ext_pair_load(V + vc0 + p, R + ro0 + p, umin_(vl - vc0 - p, rl - ro0 - p), V + vc0, R + ro0,
+				              umin_(vc0, ro0), ex);
+			}
+			if (off != kNone) {   // correcting.c:268-285: verify the seed bytes
+				if (p == 16) {
+					uint32_t wr[4];
+					ld16u(R + off, wr);
+					hit = ((wr[0] ^ wv[0]) | (wr[1] ^ wv[1]) | (wr[2] ^ wv[2]) | (wr[3] ^ wv[3])) == 0u;
+				} else {
+					hit = true;
+					for (uint32_t j = 0; j < p && hit; ++j) hit = R[off + j] == V[pos + j];
+				}
+				if (a.stats && !hit) {   // the reference's stored-fingerprint test (:254-283)
+					const bool fpeq = window_fp<0>(R + off, p, a.powc) == fp;
+					fpm = !fpeq;
+					bm = fpeq;
 				}
 			}
 			const uint64_t M = __ballot(hit);
@@ -601,8 +692,12 @@ __global__ __launch_bounds__(64) void correcting_scan_kernel(EncodeArgs a) {
 			vc = uni(vc + jf);
 			const uint32_t ro = uni(rdlane(off, jf));
 			// ── extensions (correcting.c:293-303) ──
-			const uint32_t fwd = p + uni(ext_fwd(V + vc + p, R + ro + p, umin_(vl - vc - p, rl - ro - p)));
-			const uint32_t bwd = uni(ext_bwd(V + vc, R + ro, umin_(vc, ro)));
+			uint32_t fx, bx;
+			const uint32_t flim = umin_(vl - vc - p, rl - ro - p), blim = umin_(vc, ro);
+			if (vc == vc0 && ro == ro0) ext_pair_eval(V + vc + p, R + ro + p, flim, V + vc, R + ro, blim, ex, &fx, &bx);
+			else ext_both(V + vc + p, R + ro + p, flim, V + vc, R + ro, blim, &fx, &bx);
+			const uint32_t fwd = p + uni(fx);
+			const uint32_t bwd = uni(bx);
 			const uint32_t vm = vc - bwd, rm = ro - bwd, mend = vm + bwd + fwd;
 			if (vs <= vm) {
 				// 6a: the match lies in the unencoded suffix (correcting.c:316-363)

@@ -41,9 +41,11 @@ __device__ __forceinline__ uint64_t mod_q(uint64_t x, uint64_t q, uint64_t magic
 // above needs four quarter-rate 32x32 multiplies).  x = xh 2^32 + xl with
 // xh < 2^29:
 //   y = xh (2^32 mod q) + xl         (< 2^52 + 2^32: exact in one FMA)
-//   r = y - floor(y / q) q           (in [-q, 2q), exact)
-// and two unsigned minimums bring r into [0, q).  The quotient is off by at
-// most one because y / q * 2^-52 < 1.
+//   r = y - floor(y inv) q           (exact)
+// with inv = 1/q rounded DOWN: y inv never exceeds y / q, and the product's
+// rounding (half an ulp of a quotient < 2^52 / q) stays below the 1/q gap
+// to the next integer, so floor(y inv) is the quotient or one less and r is
+// in [0, 2q): one unsigned minimum brings it into [0, q).
 struct ModQ {
 	double qd, inv, k1;   // q, 1/q, 2^32 mod q
 	bool ok;              // q < 2^23: this path applies
@@ -54,16 +56,17 @@ __device__ __forceinline__ ModQ make_modq(uint64_t q, uint64_t magic) {
 	m.ok = q < (1ull << 23);
 	m.qd = (double)q;
 	m.inv = 1.0 / m.qd;
+	if (__fma_rn(m.inv, m.qd, -1.0) > 0.0) m.inv = __longlong_as_double(__double_as_longlong(m.inv) - 1);
 	m.k1 = (double)mod_q(1ull << 32, q, magic);
 	return m;
 }
 
+// (xh converted as a signed dword, xh < 2^29: the unsigned form of
+// (x >> 32) is lowered as a 64-bit conversion, an extra ldexp + add per call)
 __device__ __forceinline__ uint32_t mod_q_small(uint64_t x, const ModQ& m) {
-	const double y = __fma_rn((double)(uint32_t)(x >> 32), m.k1, (double)(uint32_t)x);
-	const uint32_t u = (uint32_t)(int32_t)__fma_rn(-floor(y * m.inv), m.qd, y);
-	const uint32_t q = (uint32_t)m.qd;
-	const uint32_t v = min(u, u + q);
-	return min(v, v - q);
+	const double y = __fma_rn((double)(int32_t)(uint32_t)(x >> 32), m.k1, (double)(uint32_t)x);
+	const uint32_t u = (uint32_t)__fma_rn(-floor(y * m.inv), m.qd, y);
+	return min(u, u - (uint32_t)m.qd);
 }
 
 // slot = x mod q by whichever path applies (m.ok is wave-uniform)
