@@ -6,7 +6,7 @@ onepass16_kernel<false, true>), inside the same plan as the member pairs.
 Every delta is compared with the oracle: dense and sparse insertions and
 deletions, unrelated streams, a random stretch inside a shifted pair, moved
 blocks, a large insertion, V much shorter or longer than R, lengths around
-the member chunk size.
+the member chunk size, an unrelated first chunk before a diagonal rest.
 """
 import random
 
@@ -57,6 +57,14 @@ def _pairs(seed):
     out.append(("moved_blocks", R, b"".join(blocks)))
     R = rng.randbytes(150000)
     out.append(("big_insert", R, R[:30000] + rng.randbytes(20000) + R[30000:]))
+    # chunk 0 unrelated, the rest diagonal (1 % substitutions): the member
+    # kernel skips the pair's later chunks once chunk 0 verified too few
+    R = rng.randbytes(200000)
+    V = bytearray(R)
+    for k in rng.sample(range(3000, len(V)), len(V) // 100):
+        V[k] = rng.randrange(256)
+    V[:3000] = rng.randbytes(3000)
+    out.append(("bad_head", R, bytes(V)))
     R = rng.randbytes(160000)
     out.append(("v_shorter", R, _shifted(rng, R[:70000], 500, 8)))
     R = rng.randbytes(70000)
