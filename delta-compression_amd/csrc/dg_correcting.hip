@@ -242,9 +242,15 @@ __device__ uint32_t ext_from(const uint8_t* a, const uint8_t* b, uint32_t ml, ui
 
 // both extensions of a seed match: forward a[0..) vs b[0..) up to flim,
 // backward a[-1], a[-2], ... vs b[-1], ... up to blim; their first steps
-// (2 KiB each) together.  The first steps stay at the register footprint of
-// one 4 KiB step: the V CRC rows kernel runs beside this one and needs room.
-constexpr int kFwdFirst = 1, kBwdFirst = 1;
+// (kFwdFirst / kBwdFirst KiB) together, loaded with the seed verify of the
+// candidates (correcting_scan_kernel), the rest in 4 KiB steps
+#ifndef DG_EXT_FWD_FIRST
+#define DG_EXT_FWD_FIRST 1
+#endif
+#ifndef DG_EXT_BWD_FIRST
+#define DG_EXT_BWD_FIRST 1
+#endif
+constexpr int kFwdFirst = DG_EXT_FWD_FIRST, kBwdFirst = DG_EXT_BWD_FIRST;
 struct ExtPair {
 	ExtStep<kFwdFirst> f;
 	ExtStep<kBwdFirst> b;
