@@ -205,6 +205,11 @@ struct MemSerArgs {
 	uint8_t* out;
 	uint64_t out_cap;
 	int32_t* status;
+	// sparse deltas: when the whole batch's delta bytes (offsets[n_pairs], the
+	// scan's total) are under 1/8 of sum |V| (v_total), ADD payloads are read
+	// from V in HBM instead of staging every chunk's V bytes; 0 = always stage
+	uint64_t v_total;
+	uint32_t n_pairs;
 };
 
 // COPY records: (v, r, len) u32 words, and for onepass a 4th word holding the

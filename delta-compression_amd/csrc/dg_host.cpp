@@ -436,6 +436,7 @@ struct dg_encode_plan {
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
+	uint64_t v_total = 0;      // sum |V| of the batch
 	uint32_t dbg = 0;          // DG_DEBUG_BITS: kernel A/B switches (A/B builds only)
 	bool fused = false;        // DG_FUSED=1: onepass16 serialises in-kernel (default: scan + serialise)
 	// timing
@@ -817,6 +818,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		const char* rm = ab_env("DG_ROUTE_MIN");
 		P->route_min = ctx->onepass_members == 0 ? (rm ? (uint32_t)strtoul(rm, nullptr, 0) : 2u) : 0u;
 	}
+	for (uint32_t i = 0; i < n; ++i) P->v_total += pairs[i].v_len;
 	if (P->members) {
 		// chunks of kMemChunk positions covering [0, min(|R|, |V|)]; member
 		// slots per chunk; the (pair, chunk) table the member kernel's waves index
@@ -1081,6 +1083,8 @@ static MemSerArgs mem_ser_args(const dg_encode_plan_t* P, const uint8_t* d_ver, 
 	m.out = d_out;
 	m.out_cap = out_cap;
 	m.status = d_status;
+	m.v_total = P->n_groups == 1 ? P->v_total : 0;   // (groups serialise before the scan's total is known)
+	m.n_pairs = P->n;
 	return m;
 }
 

@@ -808,7 +808,7 @@ struct SerFetch {
 
 // every load unconditional (no branch for the compiler to drain before the
 // loads of the job after it are issued)
-__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
+__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F, bool direct) {
 	const uint32_t lane = lane_id();
 	const JobCursor& J = F.J;
 	F.st = a.status[J.pair];
@@ -820,8 +820,10 @@ __device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
 	F.slot0 = J.mem_base + (uint64_t)J.c * kMemChunkSlots;
 	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
 	const uint8_t* V = a.ver + J.v_off;
+	if (!direct) {
 #pragma unroll
-	for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
+		for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
+	}
 	F.r = make_uint4(0u, 0u, 0u, 0u);   // (slots 0..63 of the chunk's 129, only the bulk members')
 	if (lane < F.cnt) F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));
 	F.first = a.mem_s[F.slot0];
@@ -833,21 +835,18 @@ __device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
 // segments 2c, 2c + 1 (record runs of the chain's own epochs, the tail), so
 // all the chunks of a pair serialise at once.  Persistent waves over
 // contiguous jobs, each job's inputs loaded while the previous one is written.
-__global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint32_t n_jobs) {
-	__shared__ __attribute__((aligned(16))) uint8_t vbuf[kStage + 16];
-	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
+template <bool direct>
+__device__ __forceinline__ void member_serialize(const MemSerArgs& a, uint32_t j0, uint32_t j1, uint8_t* vbuf,
+                                                 uint8_t* stage) {
 	const uint32_t lane = lane_id();
-	const uint32_t j0 = a.job0 + (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
-	const uint32_t j1 = a.job0 + (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
-	if (j0 >= j1) return;
 	SerFetch F, N;
 	F.J.start(a, j0);
-	ser_fetch(a, F);
+	ser_fetch(a, F, direct);
 	for (uint32_t j = j0; j < j1; ++j) {
 		if (j + 1 < j1) {
 			N.J = F.J;
 			N.J.next(a);
-			ser_fetch(a, N);
+			ser_fetch(a, N, direct);
 		}
 		const uint32_t vl = F.J.vl;
 		const uint8_t* V = a.ver + F.J.v_off;
@@ -858,14 +857,22 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 				uint8_t* out = a.out + F.base;
 				if (F.J.c == 0) put_header(out, vl);
 				if (F.cnt) {
-					const int64_t g0 = (int64_t)F.J.c * kMemChunk - 16;
-					lds_order();
-#pragma unroll
-					for (uint32_t k = 0; k < kStageRows; ++k)
-						if (1024 * k + 16 * lane < kStage)
-							*(uint4*)(vbuf + 1024 * k + 16 * lane) = stage_piece(F.v[k], V, g0 + 1024 * k + 16 * lane, vl);
-					lds_order();
+					// ADD payloads from the chunk's V bytes staged in LDS, or
+					// (sparse deltas) straight from V: every payload is followed
+					// by a COPY of >= 16 bytes, so its <= 3-byte spill reads stay in V
+					int64_t g0 = (int64_t)F.J.c * kMemChunk - 16;
 					const uint8_t* vb = vbuf;
+					if (direct) {
+						g0 = 0;
+						vb = V;
+					} else {
+						lds_order();
+#pragma unroll
+						for (uint32_t k = 0; k < kStageRows; ++k)
+							if (1024 * k + 16 * lane < kStage)
+								*(uint4*)(vbuf + 1024 * k + 16 * lane) = stage_piece(F.v[k], V, g0 + 1024 * k + 16 * lane, vl);
+						lds_order();
+					}
 					uint64_t pos = F.boff;
 					uint32_t prev_end = F.first;
 					for (uint32_t t0 = 0; t0 < F.cnt; t0 += 64) {
@@ -926,6 +933,17 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 		}
 		F = N;
 	}
+}
+
+__global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint32_t n_jobs) {
+	__shared__ __attribute__((aligned(16))) uint8_t vbuf[kStage + 16];
+	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
+	const uint32_t j0 = a.job0 + (uint32_t)((uint64_t)n_jobs * blockIdx.x / gridDim.x);
+	const uint32_t j1 = a.job0 + (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / gridDim.x);
+	if (j0 >= j1) return;
+	// (uniform for the launch: the scan's total is final before this kernel)
+	if (a.v_total && uni64(a.offsets[a.n_pairs]) * 8 < a.v_total) member_serialize<true>(a, j0, j1, vbuf, stage);
+	else member_serialize<false>(a, j0, j1, vbuf, stage);
 }
 
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {
