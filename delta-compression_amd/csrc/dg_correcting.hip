@@ -581,7 +581,13 @@ struct RingEnt {
 	uint32_t vs, ve, r_off, kind;   // kind: 1 COPY, 2 ADD
 };
 
-__global__ __launch_bounds__(64, 4) void correcting_scan_kernel(EncodeArgs a) {
+// waves per SIMD the scan is compiled for: 4 holds one wave per pair of a
+// 4096-pair batch resident (DG_SCAN_WAVES=6 leaves room for the CRC, A/B)
+#ifndef DG_SCAN_WAVES
+#define DG_SCAN_WAVES 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_SCAN_WAVES, 8))) void correcting_scan_kernel(
+    EncodeArgs a) {
 	extern __shared__ RingEnt ring[];   // buf_cap + 1 entries
 	const uint32_t pair = blockIdx.x;
 	const uint32_t lane = lane_id();

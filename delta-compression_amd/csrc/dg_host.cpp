@@ -430,7 +430,7 @@ struct dg_encode_plan {
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
-	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's CRC pass before it
+	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
 	bool crc_wide = false;     // correcting: R's and V's CRC in one wide-table pass before the build
 	bool crc_wide_beside = false;   // ... or forked after the build, beside the V scan
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
@@ -907,12 +907,6 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	}
 	const char* sc = ab_env("DG_SERIAL_CRC");
 	P->serial_crc = sc && sc[0] == '1';
-	// correcting plans with R's CRC in the LDS build: V's CRC runs alone before
-	// the build.  Beside the build it slows the VALU-bound build by more than
-	// it takes (1.72 -> 2.23 ms); beside the latency-bound V scan it gets one
-	// wave per SIMD and takes 0.97 ms instead of 0.24 (C4: 779 vs 731 GiB/s,
-	// profiles/r04_experiments.md).  DG_SERIAL_CRC=0 restores the fork (A/B).
-	if (P->crc_fused && !(sc && sc[0] == '0')) P->serial_crc = true;
 	const char* db = ab_env("DG_DEBUG_BITS");
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = ab_env("DG_CRC_FIRST");
@@ -1138,7 +1132,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// (member plans keep the 8 KiB-LDS lane-contiguous pass: the row pass's
 			// 16 KiB blocks find no room beside the member kernel and trail it)
 			// (five-bit row tables, 3.25 KiB, fit beside it too)
-			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
+			// (correcting plans: V's CRC runs beside the latency-bound V scan
+			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
+			// there instead of 0.71: C4 731 -> 813 GiB/s)
+			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
 			                            DG_CRC5 || !P->members));
 		}
 		HIPCHK(ctx, rec(1, cs));
