@@ -105,3 +105,37 @@ def test_members_sparse_chunk_ends(dg, ctx_mode, orc, q):
     for (name, R, V), d in zip(pairs, got):
         assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
         assert dg.decode(R, d, ctx=ctx_mode) == V, name
+
+
+def _sparse_runs(seed):
+    """Pairs whose deltas are a few percent of V: the member serialiser then
+    reads ADD payloads straight from V (dg_members.hip, direct mode) instead of
+    staging each chunk.  Edits are runs of 1..300 bytes, so the payloads take
+    every copy path (the 4-byte head, 4-byte words, 16-byte pieces, the
+    wave-wide copy), some ending right before a chunk or stream boundary."""
+    rng = random.Random(seed)
+    out = []
+    for i in range(12):
+        L = 262144 + rng.randrange(3) * rng.randrange(1, 9000)
+        R = rng.randbytes(L)
+        V = bytearray(R)
+        for _ in range(24):
+            n = rng.choice((1, 3, 5, 9, 15, 17, 31, 64, 65, 120, 300))
+            at = rng.randrange(0, L - n - 40)
+            if rng.random() < 0.2:
+                at = 2048 * rng.randrange(1, L // 2048 - 1) - n   # ending at a chunk boundary
+            for k in range(n):
+                V[at + k] ^= 1 + rng.randrange(255)
+        out.append((f"runs_{i}", R, bytes(V)))
+    return out
+
+
+@pytest.mark.parametrize("q", [1, 97])
+def test_members_sparse_payload_runs(dg, ctx_mode, orc, q):
+    pairs = _sparse_runs(11 + q)
+    got = dg.encode_batch([(R, V) for _, R, V in pairs], "onepass", p=16, q=q, ctx=ctx_mode)
+    total = sum(len(d) for d in got)
+    assert total * 8 < sum(len(V) for _, _, V in pairs)   # a sparse batch: the direct serialiser
+    for (name, R, V), d in zip(pairs, got):
+        assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
+        assert dg.decode(R, d, ctx=ctx_mode) == V, name
