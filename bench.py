@@ -799,23 +799,24 @@ def main():
     ctx = dg.Context(local)
     stream = torch.cuda.Stream()
 
-    # Every device measurement first and the headline config's last, right
-    # after the other lines' (its inputs and plan are prepared up front), on a
-    # GPU that is already at its running clocks: from a cold start the first
-    # 20 steps of C2 read ~12 % slow (0.378 vs 0.331 ms per step over 200).
-    # Then the CPU baselines (host only).
+    # The headline config first, then the other lines, then the CPU baselines
+    # (host only).  A GPU leaving ~300 ms of idle runs ~40 C2 steps ~15 %
+    # slow (profiles/r04_fresh_plan_c2.json); each line's own untimed steps
+    # (the checked step, the stage-profile pass, W warmup: `untimed_steps`)
+    # cover that, and the headline measured first reads the same as measured
+    # last (C2 1734 / 1720 alone vs 1721 last, one box, round 4).
     extras = [c for c in args.also.split(",") if c and c != "none" and c != args.config]
     head_measure, head_release = prepare_config(args.config, args, R, dg, ctx, shard, stream)
+    line = head_measure()
+    head_release()
     also, release = {}, None
     for name in extras:
         if release:
             release()
         measure, release = prepare_config(name, args, R, dg, ctx, shard, stream)
         also[name] = measure()
-    line = head_measure()
     if release:
         release()
-    head_release()
     add_cpu_baseline(args.config, line, args, R)
     for name in extras:
         add_cpu_baseline(name, also[name], args, R)
