@@ -148,6 +148,18 @@ def main():
                "hbm_bytes_per_launch": raw_f * fac + raw_w,
                "correction": f"FETCH_SIZE KiB x 1024 x {fac:.3f} ({cls}, profiles/{tag}_pmc_calib.json); "
                              "WRITE_SIZE KiB x 1024"}
+        if cfg == "c4":
+            # the LDS build streams R (x fac, as calibrated); the scan mixes
+            # coalesced windows / extension steps with random index (4 B) and
+            # seed-verify (16 B) loads, each tallied at 64 B: x1 and x2 readings
+            scan = sum(v for k, v in f.items() if "correcting_scan" in k) * 1024
+            rest = raw_f - scan
+            res["kernels_fetch_class"] = {"build": cls, "scan": "mixed: coalesced windows + random index loads"}
+            res["fetch_bytes_per_launch"] = rest * fac + scan
+            res["hbm_bytes_per_launch"] = rest * fac + scan + raw_w
+            res["hbm_bytes_upper"] = rest * fac + scan * 2.0 + raw_w
+            res["correction"] = (f"build FETCH_SIZE x {fac:.3f} ({cls}); scan FETCH_SIZE x 1 (lower reading: "
+                                 "random requests tallied at 64 B) and x 2 in hbm_bytes_upper; WRITE_SIZE x 1")
         if table_tier:
             res["hbm_bytes_upper"] = raw_f * 2.0 + raw_w
             res["correction"] = ("FETCH_SIZE KiB x 1024 x 1 (lower reading: every request 64 B as tallied); "
