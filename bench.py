@@ -377,7 +377,8 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
 
     in_bytes_rank = sum(rl + vl for _, rl, _, vl in layout)
-    value = in_bytes_rank * R.world * args.steps / elapsed / 2**30
+    in_bytes_job = shard.sum_over_ranks(R.dist, in_bytes_rank, R.world, "cuda")
+    value = in_bytes_job * args.steps / elapsed / 2**30
     members = plan.members
     # the dominant kernel: the member kernel alone in member mode (its own
     # event pair), else the differencing kernel(s) of the "diff" stage
@@ -558,6 +559,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     stages = plan.stage_times()
     elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
     v_bytes = sum(vl for _, _, _, vl in layout)
+    v_bytes_job = shard.sum_over_ranks(R.dist, v_bytes, R.world, "cuda")
     d_bytes = d_offs[-1]
     dec_ms = stages.get("decode", 0.0)
     # decode algorithmic bytes: every delta byte read, R read
@@ -574,7 +576,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     traffic, traffic_src = pmc_traffic(name, "decode_kernel") if npg == CONFIGS[name][0] else (None, None)
     line = {
         "metric": "delta-decode GiB/s (device-resident, sum |V| reconstructed, CRC-verified)",
-        "value": round(v_bytes * R.world * args.steps / elapsed / 2**30, 3),
+        "value": round(v_bytes_job * args.steps / elapsed / 2**30, 3),
         "unit": "GiB/s", "n_gpus": R.world, "steps": args.steps, "warmup": args.warmup,
         "untimed_steps": 1 + args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -607,6 +609,90 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     plan.close()
     del ref, ver, out, d_dev, out_len, status
     torch.cuda.empty_cache()
+
+
+E2E_PAIRS, E2E_CHUNK_PAIRS = 16384, 1024
+
+
+def bench_e2e(args, R, dg, ctx, stream):
+    """The PCIe-inclusive rate (north_star): 16384 C2
+    pairs (4 x the C2 batch, 2 GiB of R + V) in pinned host memory, encoded
+    host to host by dg_encode_pipelined (1024-pair chunks, two in flight: H2D
+    of chunk i+1 and D2H of chunk i-1's delta bytes overlap the encode of
+    chunk i; main.c:249-292 per pair in the reference).  value = sum(|R|+|V|)
+    / wall time of one call (median of K calls after a warm-up call); beside
+    it the H2D-only rate of the same pinned arenas."""
+    import ctypes as C
+    torch = R.torch
+    npg, L, rate, q, seed_base = CONFIGS["c2"][:5]
+    n = E2E_PAIRS
+    ref_d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ver_d = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ctx.check(dg.lib.dg_synth_edit_pairs_device(ctx.handle, ref_d.data_ptr(), ver_d.data_ptr(), n, L, seed_base,
+                                                int(rate * L + 0.5), stream.cuda_stream), "synth")
+    torch.cuda.synchronize()
+    ref_h = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    ver_h = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    ref_h.copy_(ref_d)
+    ver_h.copy_(ver_d)
+    p = 16
+    cap = n * (35 + L + (L // p) * (22 - p))   # the plan's output bound per pair (onepass)
+    out_h = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+    L_ = dg._lib
+    pa = (L_.Pair * n)(*[L_.Pair(i * L, L, i * L, L) for i in range(n)])
+    offs = (C.c_uint64 * (n + 1))()
+    st = (C.c_int32 * n)()
+    o = L_.DiffOptions.make(q=q)
+    chunk = 2 * L * E2E_CHUNK_PAIRS
+
+    def call():
+        ctx.check(dg.lib.dg_encode_pipelined(ctx.handle, 1, ref_h.data_ptr(), ver_h.data_ptr(), pa, n, C.byref(o),
+                                             chunk, out_h.data_ptr(), cap, offs, st), "dg_encode_pipelined")
+
+    call()   # plans, device buffers, pinned staging
+    bad = sum(1 for i in range(n) if st[i])
+    if bad:
+        raise SystemExit(f"e2e_c2: {bad} pairs failed")
+    # spot check: the same bytes as the device-resident C2 plan's (checked by
+    # the parity suite) through the one-pair entry point
+    ob = out_h.numpy()
+    rh, vh = ref_h.numpy(), ver_h.numpy()
+    for i in range(0, n, n // 4 + 1):
+        want = dg.encode(rh[i * L:(i + 1) * L].tobytes(), vh[i * L:(i + 1) * L].tobytes(), "onepass", q=q)
+        if ob[offs[i]:offs[i + 1]].tobytes() != want:
+            raise SystemExit(f"e2e_c2: pair {i} differs from dg_encode")
+    reps = max(3, min(args.steps, 7))
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    h2d = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            ref_d.copy_(ref_h, non_blocking=True)
+            ver_d.copy_(ver_h, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d.append(time.perf_counter() - t0)
+    h2d.sort()
+    in_bytes = 2 * n * L
+    line = {
+        "metric": "host-to-host delta-encode GiB/s (dg_encode_pipelined, pinned host arenas)",
+        "value": round(in_bytes / med / 2**30, 3), "unit": "GiB/s", "n_gpus": 1, "calls": reps,
+        "ms_per_call": round(med * 1e3, 3), "min_ms": round(ts[0] * 1e3, 3),
+        "h2d_gibs": round(in_bytes / h2d[len(h2d) // 2] / 2**30, 3),
+        "h2d_note": "R and V arenas pinned host -> device alone (torch copy_, one stream), median of 3",
+        "config": {"workload": f"{n} C2 pairs (64 KiB, 1% edits, --table-size 1) host to host",
+                   "pairs": n, "pair_bytes": L, "chunk_pairs": E2E_CHUNK_PAIRS,
+                   "delta_bytes": int(offs[n])},
+    }
+    del ref_d, ver_d, ref_h, ver_h, out_h
+    torch.cuda.empty_cache()
+    return line
 
 
 def prepare_config(name, args, R, dg, ctx, shard, stream):
@@ -660,6 +746,9 @@ def _roof_short(r):
 
 def also_entry(line):
     """One config of the run in a few numbers (the full line is in the file)."""
+    if "roofline" not in line:   # the host-to-host line (bench_e2e)
+        return {"value": line["value"], "ms_per_call": line["ms_per_call"], "h2d_gibs": line["h2d_gibs"],
+                "metric": "e2e"}
     r = line["roofline"]
     e = {"value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": r.get("avg_launch_ms"),
          "frac": r.get("frac"), "path_frac": r.get("path_frac")}
@@ -749,10 +838,18 @@ def dry_run(args, world, rank):
     off = gather.global_offsets(gather(dist, sizes))
     elapsed = shard.max_over_ranks(dist, time.perf_counter() - t0, world, "cpu")
     ok = int(off[-1]) == sum(range(total)) + 26 * total
+    # the job's bytes as the timed lines count them: every rank's own sum,
+    # all-reduced (the ranges are unequal, so rank 0's bytes x world is not it)
+    pair_bytes = [1000 * (1 + i % 7) for i in range(total)]
+    bytes_rank = sum(pair_bytes[lo:hi])
+    bytes_job = shard.sum_over_ranks(dist, bytes_rank, world, "cpu")
+    ok = ok and bytes_job == sum(pair_bytes)
     if rank == 0:
         print(json.dumps({"metric": "launcher dry run (no GPU, no encode)", "value": None,
                           "n_gpus": world, "steps": 0, "warmup": 0, "ranges": allr,
-                          "index_ok": ok, "elapsed_s": elapsed}), flush=True)
+                          "index_ok": ok, "elapsed_s": elapsed, "bytes_job": bytes_job,
+                          "bytes_expected": sum(pair_bytes), "bytes_rank0_x_world": bytes_rank * world}),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -770,6 +867,8 @@ def main():
                          "('none' to skip)")
     ap.add_argument("--pairs", type=int, default=0, help="override pairs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip the host-to-host line (also.e2e_c2: dg_encode_pipelined, 16384 pinned C2 pairs)")
     ap.add_argument("--full-out", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
                     help="where the full detail of every line goes (the printed line is compact)")
     ap.add_argument("--dry-run", action="store_true",
@@ -817,17 +916,19 @@ def main():
         also[name] = measure()
     if release:
         release()
+    if args.e2e and world == 1:
+        also["e2e_c2"] = bench_e2e(args, R, dg, ctx, stream)
     add_cpu_baseline(args.config, line, args, R)
     for name in extras:
         add_cpu_baseline(name, also[name], args, R)
     if rank == 0:
-        full = dict(line, also=also) if extras else line
+        full = dict(line, also=also) if also else line
         path = args.full_out
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         with open(path, "w") as f:
             json.dump(full, f, indent=1)
         print(f"bench.py: every field of every line in {path}", file=sys.stderr, flush=True)
-        print(compact_line(line, also if extras else None, os.path.relpath(path, ROOT)), flush=True)
+        print(compact_line(line, also or None, os.path.relpath(path, ROOT)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

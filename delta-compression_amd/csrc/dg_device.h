@@ -73,26 +73,19 @@ constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
 // lanes x^(8 * 256), x^(8 * 512) (its first two tree levels) and x^(8 * 48 KiB)
 constexpr int kCrcFinTabs = 1 + 16 + 3 + 3;
 constexpr int kCrcFinX256 = 20, kCrcFinX512 = 21, kCrcFinX48K = 22;   // indices in F
-// after F: the row-interleaved segment tables (crc_seg_rows): for 16- and
-// 8-byte pieces, U_j = T advanced by (64 PB - 1 - j) bytes (16 and 8 tables
-// of 256), then the per-lane constants x^(-8 PB l), l = 0..63, for PB = 16, 8
+// after F: the row-interleaved segment tables (dg_crc.h crc_seg_rows): for
+// 16- and 8-byte pieces, U_j = T advanced by (64 PB - 1 - j) bytes (16 and 8
+// tables of 256), then the per-lane constants x^(-8 PB l), l = 0..63, for PB
+// = 16, 8; then the five-bit row tables F_k[v] = Z^n(v << 5k), k = 0..12, 32
+// entries (256 B: one LDS row, so a 32-lane ds_read_b64 group never
+// conflicts) -- for 8-byte pieces n = 512; for 16-byte pieces n = 1024 on
+// (A ^ low 8 bytes), then 13 more with n = 1016 on the high 8 bytes
 constexpr uint32_t kCrcRowsOff = 8 * 256 + (kCrcLevels + kCrcFinTabs) * kCrcNibTabWords;
 constexpr uint32_t kCrcRows16 = kCrcRowsOff, kCrcRows8 = kCrcRowsOff + 16 * 256;
 constexpr uint32_t kCrcRowK16 = kCrcRowsOff + 24 * 256, kCrcRowK8 = kCrcRowK16 + 64;
-// then the five-bit row tables (crc_seg_rows5): F_k[v] = Z^n(v << 5k), k = 0..12,
-// 32 entries (256 B: one LDS row, so a 32-lane ds_read_b64 group never
-// conflicts) -- for 8-byte pieces n = 512; for 16-byte pieces n = 1024 on
-// (A ^ low 8 bytes), then 13 more with n = 1016 on the high 8 bytes
 constexpr uint32_t kCrc5Tabs8 = 13, kCrc5Tabs16 = 26;
-#ifndef DG_CRC5
-#define DG_CRC5 0   // 1: the encode's row passes use the five-bit tables (A/B; byte tables by default)
-#endif
-#ifndef DG_DEC_CRC
-#define DG_DEC_CRC 1   // decode kernel CRCs: 0 lane-contiguous segments at the end (R read twice),
-#endif                 // 1 byte-table rows with R's CRC from the in-place fill, 2 the same on five-bit tables
 constexpr uint32_t kCrc5R8 = kCrcRowK8 + 64, kCrc5R16 = kCrc5R8 + 32 * kCrc5Tabs8;
 constexpr uint32_t kCrcTabWords = kCrc5R16 + 32 * kCrc5Tabs16;
-
 
 struct EncodeArgs {
 	const uint8_t* ref;
@@ -280,6 +273,7 @@ const char* ab_env(const char* name);
 // the context's slot for the pipelined host path's state, and its destructor
 void** ctx_io(dg_context_t* ctx, void (*release)(void*));
 uint64_t ctx_limits_gen(const dg_context_t* ctx);   // changes with every dg_context_set_limit
+int ctx_device(const dg_context_t* ctx);            // the context's HIP device
 // --verbose: the reference's diagnostic lines for pair i of a plan to stderr,
 // from the plan's parameters, its 8 device counters (copied to the host; may
 // be NULL for onepass) and the pair's delta (dg_host.cpp)
@@ -300,10 +294,14 @@ hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
-// rows: the row-interleaved pass (16 KiB LDS per block) instead of the
-// lane-contiguous one (8 KiB)
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, bool rows = true);
-// the CRC with bank-spread tables in 128 KiB of LDS: for a pass that has the GPU to itself
+// pass: the row-interleaved pass on byte tables (16 KiB LDS per block), on
+// five-bit tables (3.25 KiB), or the lane-contiguous pass (8 KiB)
+enum : int { kCrcPassRows = 0, kCrcPassRows5 = 1, kCrcPassLanes = 2 };
+#ifndef DG_CRC_MEMBERS
+#define DG_CRC_MEMBERS 2   // the pass beside the member kernel (A/B: make variant)
+#endif
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, int pass = kCrcPassRows);
+// the CRC on 16-byte pieces (32 KiB of tables): for a pass that has the GPU to itself
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_synth(uint8_t* ref, uint8_t* ver, uint32_t n_pairs, uint64_t pair_len,

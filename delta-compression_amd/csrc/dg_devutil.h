@@ -304,21 +304,58 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 	return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
 
+// ── 3-input XOR (gfx950 v_bitop3_b32, truth table 0x96) ──
+// The compiler fuses AND/OR/XOR mixes into v_bitop3 but not XOR chains, so
+// table folds (CRC, GF(2) products) build their XORs as explicit trees: N
+// terms cost ceil((N - 1) / 2) instructions instead of N - 1.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+	return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+template <int N>
+__device__ __forceinline__ uint32_t xor_tree(const uint32_t* v) {
+	if constexpr (N == 1) {
+		return v[0];
+	} else if constexpr (N == 2) {
+		return v[0] ^ v[1];
+	} else {
+		constexpr int M = (N + 2) / 3;
+		uint32_t w[M];
+#pragma unroll
+		for (int i = 0; i < M; ++i) {
+			if (3 * i + 2 < N) w[i] = xor3(v[3 * i], v[3 * i + 1], v[3 * i + 2]);
+			else if (3 * i + 1 < N) w[i] = v[3 * i] ^ v[3 * i + 1];
+			else w[i] = v[3 * i];
+		}
+		return xor_tree<M>(w);
+	}
+}
+template <int N>
+__device__ __forceinline__ uint64_t xor_tree64(const uint64_t* v) {
+	uint32_t l[N], h[N];
+#pragma unroll
+	for (int k = 0; k < N; ++k) {
+		l[k] = (uint32_t)v[k];
+		h[k] = (uint32_t)(v[k] >> 32);
+	}
+	return ((uint64_t)xor_tree<N>(h) << 32) | xor_tree<N>(l);
+}
+
 // ── CRC-64/XZ helpers (reflected representation: bit 63 = x^0) ──
 
 // c * K mod P by the constant's nibble tables (tab[16 j + n] = (n x^(4 j)) K)
 __device__ __forceinline__ uint64_t mul_nib(uint64_t c, const uint64_t* __restrict__ tab) {
-	uint64_t r = 0;
+	uint64_t v[16];
 #pragma unroll
-	for (int j = 0; j < 16; ++j) r ^= tab[16 * j + ((c >> (4 * j)) & 15)];
-	return r;
+	for (int j = 0; j < 16; ++j) v[j] = tab[16 * j + ((c >> (4 * j)) & 15)];
+	return xor_tree64<16>(v);
 }
 
 // slicing-by-4 step: the register's low 32 bits absorb one little-endian word
 __device__ __forceinline__ uint64_t slice4(uint64_t crc, uint32_t w, const uint64_t* __restrict__ T) {
 	const uint64_t x = crc ^ w;
-	return T[3 * 256 + (x & 0xff)] ^ T[2 * 256 + ((x >> 8) & 0xff)] ^ T[256 + ((x >> 16) & 0xff)] ^
-	       T[(x >> 24) & 0xff] ^ (x >> 32);
+	const uint64_t v[5] = {T[3 * 256 + (x & 0xff)], T[2 * 256 + ((x >> 8) & 0xff)], T[256 + ((x >> 16) & 0xff)],
+	                       T[(x >> 24) & 0xff], x >> 32};
+	return xor_tree64<5>(v);
 }
 
 // a * b mod P, bit-serial (64 steps; for products by a per-lane constant)

@@ -121,6 +121,7 @@ struct dg_context {
 };
 
 uint64_t dg::ctx_limits_gen(const dg_context_t* ctx) { return ctx->limits_gen; }
+int dg::ctx_device(const dg_context_t* ctx) { return ctx->device; }
 
 void** dg::ctx_io(dg_context_t* ctx, void (*release)(void*)) {
 	ctx->io_free = release;
@@ -1129,14 +1130,15 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
 		if (!P->skip_crc) {
 			if (P->crc_wide) HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, cs));
-			// (member plans keep the 8 KiB-LDS lane-contiguous pass: the row pass's
-			// 16 KiB blocks find no room beside the member kernel and trail it)
-			// (five-bit row tables, 3.25 KiB, fit beside it too)
+			// (member plans: the lane-contiguous pass, 8 KiB of LDS.  The byte-table
+			// row pass's 16 KiB blocks find no room beside the member kernel and
+			// trail it; the five-bit row pass (3.25 KiB) finishes sooner but its
+			// VALU slows the member kernel: C3 -2.5 %, c6 +5 %, round 5)
 			// (correcting plans: V's CRC runs beside the latency-bound V scan
 			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
 			// there instead of 0.71: C4 731 -> 813 GiB/s)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            DG_CRC5 || !P->members));
+			                            P->members ? DG_CRC_MEMBERS : kCrcPassRows));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;

@@ -338,22 +338,34 @@ int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algo
 		}
 	}
 	{
+		// one host thread per context (dg_encode_pipelined makes the thread's
+		// current device the context's); a thread that cannot be started runs
+		// its range on the calling thread after the others are joined
+		auto work = [&](uint32_t d) {
+			Range& r = R[d];
+			if (r.hi == r.lo) {
+				r.off[0] = 0;
+				return;
+			}
+			r.rc = dg_encode_pipelined(ctxs[d], algo, h_ref, h_ver, pairs + r.lo, r.hi - r.lo, opts, chunk_bytes,
+			                           r.out.data(), r.out.size(), r.off.data(), r.st.data());
+		};
 		std::vector<std::thread> th;
-		for (uint32_t d = 0; d < D; ++d)
-			th.emplace_back([&, d] {
-				Range& r = R[d];
-				if (r.hi == r.lo) {
-					r.off[0] = 0;
-					return;
-				}
-				r.rc = dg_encode_pipelined(ctxs[d], algo, h_ref, h_ver, pairs + r.lo, r.hi - r.lo, opts, chunk_bytes,
-				                           r.out.data(), r.out.size(), r.off.data(), r.st.data());
-			});
+		uint32_t started = 0;
+		try {
+			th.reserve(D);
+			for (; started < D; ++started) th.emplace_back(work, started);
+		} catch (...) {   // std::system_error / bad_alloc: no exception crosses the C ABI
+		}
 		for (auto& t : th) t.join();
+		for (uint32_t d = started; d < D; ++d) work(d);
 	}
-	// pack in pair order
+	// pack in pair order, as dg_encode_pipelined does: once a pair's delta
+	// does not fit, it and every later pair report DG_ERR_CAPACITY (a pair
+	// the device failed keeps its own status) at the bytes written so far
 	uint64_t pos = 0;
 	int rc_all = DG_OK;
+	bool full = false;
 	out_offsets[0] = 0;
 	for (uint32_t d = 0; d < D; ++d) {
 		Range& r = R[d];
@@ -366,24 +378,26 @@ int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algo
 			if (rc_all == DG_OK) rc_all = r.rc;
 			continue;
 		}
-		const uint64_t bytes = r.off[m];
-		if (pos + bytes > out_cap) {   // h_out is full from here on
-			for (uint32_t k = 0; k < m; ++k) {
-				out_offsets[r.lo + k + 1] = pos;
+		uint32_t fit = 0;   // this range's leading pairs that fit
+		if (!full) {
+			while (fit < m && pos + r.off[fit + 1] <= out_cap) ++fit;
+			if (fit < m) full = true;
+		}
+		par_memcpy(h_out + pos, r.out.data(), r.off[fit]);
+		for (uint32_t k = 0; k < m; ++k) {
+			if (k < fit) {
+				out_offsets[r.lo + k + 1] = pos + r.off[k + 1];
+				if (status) status[r.lo + k] = r.st[k];
+				if (!status && r.st[k] != DG_OK && rc_all == DG_OK) rc_all = r.st[k];
+			} else {
+				out_offsets[r.lo + k + 1] = pos + r.off[fit];
 				if (status) status[r.lo + k] = r.st[k] != DG_OK ? r.st[k] : DG_ERR_CAPACITY;
 			}
-			rc_all = DG_ERR_CAPACITY;
-			continue;
 		}
-		par_memcpy(h_out + pos, r.out.data(), bytes);
-		for (uint32_t k = 0; k < m; ++k) {
-			out_offsets[r.lo + k + 1] = pos + r.off[k + 1];
-			if (status) status[r.lo + k] = r.st[k];
-			if (!status && r.st[k] != DG_OK && rc_all == DG_OK) rc_all = r.st[k];
-		}
-		pos += bytes;
+		pos += r.off[fit];
 	}
-	return rc_all;
+	if (full) return DG_ERR_CAPACITY;
+	return status ? DG_OK : rc_all;
 }
 
 int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h_ref, const uint8_t* h_ver,
@@ -394,6 +408,9 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 	out_offsets[0] = 0;
 	if (n == 0) return DG_OK;
 	if (opts && ((opts->flags >> DG_OPT_INPLACE) & 1)) return DG_ERR_UNSUPPORTED;   // host step: dg_encode_batch
+	// the calling thread's current device becomes the context's before any
+	// stream or event of it is made (a new host thread starts on device 0)
+	if (hipSetDevice(dg::ctx_device(ctx)) != hipSuccess) return DG_ERR_HIP;
 	dg_diff_options_t o;
 	if (opts) o = *opts; else dg_diff_options_default(&o);
 	if (chunk_bytes == 0) chunk_bytes = 256ull << 20;

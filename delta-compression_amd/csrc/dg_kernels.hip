@@ -17,6 +17,7 @@
 
 #include "dg_device.h"
 #include "dg_devutil.h"
+#include "dg_crc.h"
 #include "dg_serialize_wave.h"
 
 namespace dg {
@@ -80,94 +81,55 @@ __device__ __forceinline__ void put_u32be(uint8_t* o, uint32_t x) {
 
 // ───────────────────────────── CRC-64/XZ ──────────────────────────────────
 //
-// Tables (built on the host, uploaded once per context):
+// Tables (built on the host, uploaded once per context; dg_device.h):
 //   slice[8][256]    slicing-by-8 tables of the reflected polynomial
 //   lvl[6][256]      nibble tables of "multiply by x^(8*L*2^l) mod P",
-//                    L = kCrcLaneBytes, for the in-wave combine tree
+//                    L = kCrcLaneBytes, for the lane-contiguous in-wave tree
+//   the row tables and per-lane constants of dg_crc.h
 // The raw CRC (init 0, no xorout) is linear, leading zero bytes are no-ops
 // and init = ~0 equals XOR-ing 0xFF into the first 8 data bytes, so each
-// lane hashes an equal-length chunk of a zero-front-padded span and the
-// chunks are combined as c_left * x^(8*len_right) ^ c_right.
+// segment is hashed from a zero register over a zero-front-padded span and
+// the segments are combined as c_left * x^(8*len_right) ^ c_right.
 
-
-
-__device__ __forceinline__ uint64_t slice8(uint64_t x, const uint64_t* __restrict__ T) {
-	return T[7 * 256 + (x & 0xff)] ^ T[6 * 256 + ((x >> 8) & 0xff)] ^
-	       T[5 * 256 + ((x >> 16) & 0xff)] ^ T[4 * 256 + ((x >> 24) & 0xff)] ^
-	       T[3 * 256 + ((x >> 32) & 0xff)] ^ T[2 * 256 + ((x >> 40) & 0xff)] ^
-	       T[1 * 256 + ((x >> 48) & 0xff)] ^ T[0 * 256 + (x >> 56)];
-}
-
-
-// keep-mask of bytes [lo, hi) within an 8-byte word (0 <= lo, hi <= 8)
-__device__ __forceinline__ uint64_t byte_mask(int lo, int hi) {
-	lo = lo < 0 ? 0 : lo;   // clamp first: a negative shift count is undefined
-	hi = hi > 8 ? 8 : hi;   // (gfx950 would use its low 6 bits)
-	if (hi <= lo) return 0;
-	const uint64_t up = hi == 8 ? ~0ULL : ((1ULL << (8 * hi)) - 1);
-	const uint64_t dn = lo == 0 ? 0ULL : ((1ULL << (8 * lo)) - 1);
-	return up & ~dn;
-}
-
-
-// The raw CRC (init 0) of segment j of nseg (64 LB bytes each) of the span
-// [start, start + len) (len >= 8; the span's first 8 bytes inverted: init =
-// ~0) by one wave: each lane folds LB bytes, then an in-wave tree.  Uniform
-// result.  T: the slicing-by-4 tables (LDS); tree: the tree's nibble tables,
-// level l = x^(8 LB 2^l) at tree + 256 l (the context's level tables for
-// 1 KiB lanes; an LDS copy in the decode kernel).
-// The slicing tables live in LDS at byte address tb: entry (t, b) at
-// tb + TS t + BS b (TS = 2048, BS = 8 for one plain copy; the bank-spread
-// copies of crc_segments_wide_kernel: TS = 32 Ki, BS = 128, tb + 8 (lane % 16)).
-// 32-bit LDS addresses with the table offsets in the instruction's offset
-// field, and the byte extracts as SDWA shifts: ~3.75 VALU per byte (a
-// generic-pointer version compiled to ~11, 64-bit address arithmetic and
-// if-converted edge masks in every word).
-typedef const __attribute__((address_space(3))) uint64_t lds_cu64;
-__device__ __forceinline__ uint64_t ldsq(uint32_t a) { return *(lds_cu64*)(size_t)a; }
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-	return (uint32_t)(size_t)(lds_cu64*)(const uint64_t*)p;
-}
-// tbh = tb + 2 TS, a second base so every table offset fits the 16-bit
-// offset field of ds_read_b64 (the spread tables span 128 KiB).
-template <uint32_t TS, uint32_t BS>
-__device__ __forceinline__ uint64_t slice4_lds(uint64_t crc, uint32_t w, uint32_t tb, uint32_t tbh) {
+// ── lane-contiguous segments (member plans: 8 KiB of LDS) ──
+//
+// The raw CRC of segment j (64 LB bytes) by one wave: lane l folds LB
+// contiguous bytes with slicing-by-4 tables in LDS at tb (entry (t, b) at tb
+// + 2048 t + 8 b), then an in-wave tree combines the lanes (level l multiplies
+// by x^(8 LB 2^l): the context's level tables at tree + 256 l).  Each 16-byte
+// load instruction of a wave touches 64 cache lines, the reason the row form
+// (dg_crc.h) is used wherever its 16 KiB of tables fit.
+__device__ __forceinline__ uint64_t slice4_lds(uint64_t crc, uint32_t w, uint32_t tb) {
 	const uint32_t x = (uint32_t)crc ^ w;
-	return ldsq(tbh + TS + (x & 0xff) * BS) ^ ldsq(tbh + ((x >> 8) & 0xff) * BS) ^
-	       ldsq(tb + TS + ((x >> 16) & 0xff) * BS) ^ ldsq(tb + (x >> 24) * BS) ^ (crc >> 32);
+	const uint64_t v[5] = {ldsq(tb + 3 * 2048 + (x & 0xff) * 8), ldsq(tb + 2 * 2048 + ((x >> 8) & 0xff) * 8),
+	                       ldsq(tb + 2048 + ((x >> 16) & 0xff) * 8), ldsq(tb + (x >> 24) * 8), crc >> 32};
+	return xor_tree64<5>(v);
 }
 
-#ifndef DG_CRC_WIDE_PF
-#define DG_CRC_WIDE_PF 4
-#endif
-template <uint32_t LB = kCrcLaneBytes, bool kSpread = false, int kPf = 4>
 __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
                                                  uint32_t tb, const uint64_t* tree) {
-	constexpr uint32_t kLaneBytes = LB;
-	constexpr uint64_t kSeg = 64ull * LB;
-	constexpr uint32_t TS = kSpread ? 32768u : 2048u, BS = kSpread ? 128u : 8u;
+	constexpr uint32_t kLaneBytes = kCrcLaneBytes;
+	constexpr uint64_t kSeg = 64ull * kLaneBytes;
+	constexpr int kPf = 4;   // 16-byte loads in flight per lane
 	const uint32_t lane = lane_id();
 	const uintptr_t end = start + len;
 	const uintptr_t a0 = start & ~(uintptr_t)15;
 	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
 	const uintptr_t dom = a1 - (uintptr_t)nseg * kSeg;   // may wrap below a0
 	const uintptr_t cs = dom + (uintptr_t)j * kSeg + (uintptr_t)lane * kLaneBytes;
-
 	uint64_t reg = 0;
-	// kPf: 16-byte loads in flight per lane
-	// The span's first and last byte relative to the lane's chunk, clamped
-	// to a range that keeps every per-block test in 32-bit arithmetic
-	// (outside [-64, 1024 + 64] they only mean "before" / "after").
 	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 	typedef __attribute__((address_space(1))) const v4u gcu128;   // global, not flat: loads
 	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
+	// The span's first and last byte relative to the lane's chunk, clamped
+	// to a range that keeps every per-block test in 32-bit arithmetic
+	// (outside [-64, 1024 + 64] they only mean "before" / "after").
 	auto clamp32 = [](intptr_t v) -> int32_t {
 		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kLaneBytes + 64 ? (intptr_t)kLaneBytes + 64 : v));
 	};
 	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
 	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
 	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
-	const uint32_t tbh = __builtin_amdgcn_readfirstlane(0u) + tb + 2 * TS;
 	for (uint32_t w0 = 0; w0 < kLaneBytes; w0 += 16 * kPf) {
 		v4u xs[kPf];
 #pragma unroll
@@ -194,10 +156,10 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 				hi ^= byte_mask(fc - 8, fc);
 				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 			}
-			reg = slice4_lds<TS, BS>(reg, x.x, tb, tbh);
-			reg = slice4_lds<TS, BS>(reg, x.y, tb, tbh);
-			reg = slice4_lds<TS, BS>(reg, x.z, tb, tbh);
-			reg = slice4_lds<TS, BS>(reg, x.w, tb, tbh);
+			reg = slice4_lds(reg, x.x, tb);
+			reg = slice4_lds(reg, x.y, tb);
+			reg = slice4_lds(reg, x.z, tb);
+			reg = slice4_lds(reg, x.w, tb);
 		}
 	}
 	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
@@ -213,336 +175,16 @@ __device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, 
 	return uni64(reg);
 }
 
-// The same segments with the slicing tables in 16 copies spread over the LDS
-// banks (128 KiB, one 1024-thread block per CU): entry (t, b) of copy c sits
-// at byte 32 Ki t + 128 b + 8 c, i.e. on bank pair 16 (b & 1) + c, and lane
-// l reads copy l % 16, so of a 32-lane group only lanes l and l + 16 can meet
-// on a bank pair (half the time): ~2 LDS cycles per lookup instead of the
-// ~3.5 of random reads from one copy.  For a CRC pass that has the GPU to
-// itself (correcting plans: before the R-index build).
-constexpr uint32_t kCrcWideBlock = 1024;
-__global__ __launch_bounds__(kCrcWideBlock) void crc_segments_wide_kernel(CrcArgs a) {
-	extern __shared__ uint64_t TW[];   // 4 tables x 256 x 16 copies
-	for (uint32_t i = threadIdx.x; i < 4 * 256 * 16; i += kCrcWideBlock) TW[i] = a.tables[i >> 4];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6;
-	const uint32_t tb = lds_addr(TW) + 8u * (lane_id() & 15u);   // this lane's copy
-	constexpr uint32_t kWaves = kCrcWideBlock / 64;
-	for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
-		const CrcSegDev sd = a.segs[seg];
-		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_wave<kCrcLaneBytes, true, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg,
-		                                                     sd.j, tb, a.tables + 8 * 256);
-		if (lane_id() == 0) a.seg_crc[seg] = c;
-	}
-}
-
-// ── row-interleaved segments (coalesced loads) ──
-//
-// The lane-contiguous layout above gives each lane its own 1 KiB of the
-// segment, so every 16-byte load instruction of a wave touches 64 cache
-// lines (the TCP stalls on pending misses; rocprofv3: TCP_PENDING_STALL_CYCLES
-// ~45 % of the kernel at C4).  Here the segment is read as rows of 64 PB-byte
-// pieces, lane l taking piece l of every row, so one load instruction reads
-// 64 PB contiguous bytes.  Lane l folds its column Horner-wise:
-//   A <- sum_j U_j[byte j of (A ^ piece)],
-// U_j = T advanced by (64 PB - 1 - j) bytes — byte j of the piece followed
-// by the rest of its row (the other lanes' pieces) as zeros — so a piece costs
-// PB table lookups like slicing-by-PB, the 64 PB - PB byte advance folded into
-// the tables.  After the last row A_l holds lane l's bytes advanced PB * l
-// bytes too far (the row tail after its piece is 63 PB - PB l bytes, not 63
-// PB); one product by the per-lane constant x^(-8 PB l) fixes that, and the
-// segment's register is the XOR over the lanes (no combine tree).  Zeros
-// before the span leave A at 0; init = ~0 inverts the span's first 8 bytes;
-// the pad after it is undone by the finaliser, as for the layout above.
-//
-// Tables in LDS: NC copies interleaved per entry, entry (j, b) of copy c at
-// tb + 2048 NC j + 8 NC b + 8 c; lane l reads copy l % NC (NC = 4: 8 lanes
-// of a 32-lane group per copy over 8 bank pairs instead of 32 lanes over 32);
-// tables j >= 8 from tbh = tb + 8 * 2048 NC (ds_read offsets are 16-bit).
-// SEG: segment bytes; kCopy (PB = 8): pieces wholly inside [start, copy_hi)
-// are also stored at their address + copy_delta (as crc_seg_rows5).
-template <uint32_t PB, uint32_t NC, int kPf, uint32_t SEG = kCrcSegBytes, bool kCopy = false>
-__device__ __forceinline__ uint64_t crc_seg_rows(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                 uint32_t tb, uint32_t tbh, uint64_t klane,
-                                                 intptr_t copy_delta = 0, uintptr_t copy_hi = 0) {
-	static_assert(PB == 8 || PB == 16, "piece bytes");
-	static_assert(!kCopy || PB == 8, "copy: 8-byte pieces");
-	constexpr uint32_t RB = 64 * PB, NR = SEG / RB;
-	constexpr uint32_t TS = 2048 * NC, BS = 8 * NC;
-	static_assert(NR % kPf == 0, "rows per prefetch batch");
-	const uint32_t lane = lane_id();
-	const uintptr_t end = start + len;
-	const uintptr_t a0 = start & ~(uintptr_t)15;
-	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)nseg * SEG;   // may wrap below a0
-	const uintptr_t p0 = dom + (uintptr_t)j * SEG + (uintptr_t)lane * PB;
-	// span edges relative to the lane's row-0 piece, clamped so the per-row
-	// tests stay in 32-bit arithmetic
-	auto clamp32 = [](intptr_t v) -> int32_t {
-		return (int32_t)(v < -(intptr_t)RB ? -(intptr_t)RB
-		                 : (v > (intptr_t)(SEG + RB) ? (intptr_t)(SEG + RB) : v));
-	};
-	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)p0);
-	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)p0);
-	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)p0);
-	auto L = [&](uint32_t t, uint32_t b) -> uint64_t {
-		return t < 8 ? ldsq(tb + t * TS + b * BS) : ldsq(tbh + (t - 8) * TS + b * BS);
-	};
-	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-	typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-	typedef __attribute__((address_space(1))) const v4u gv4;
-	typedef __attribute__((address_space(1))) const v2u gv2;
-	uint64_t A = 0;
-	for (uint32_t r0 = 0; r0 < NR; r0 += kPf) {
-		v4u xs[kPf];
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)((r0 + u) * RB);
-			xs[u] = v4u{0, 0, 0, 0};
-			if (o + (int32_t)PB > z0) {   // pieces wholly before the span: zeros, no load
-				if constexpr (PB == 16) {
-					xs[u] = *reinterpret_cast<gv4*>(p0 + (uintptr_t)(r0 + u) * RB);
-				} else {
-					const v2u h = *reinterpret_cast<gv2*>(p0 + (uintptr_t)(r0 + u) * RB);
-					xs[u].x = h.x;
-					xs[u].y = h.y;
-				}
-			}
-		}
-		if constexpr (kCopy) {
-#pragma unroll
-			for (int u = 0; u < kPf; ++u) {
-				const uintptr_t pa = p0 + (uintptr_t)(r0 + u) * RB;
-				if (pa >= start && pa + PB <= copy_hi)
-					*reinterpret_cast<__attribute__((address_space(1))) v2u*>(pa + copy_delta) = v2u{xs[u].x, xs[u].y};
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)((r0 + u) * RB);
-			v4u x = xs[u];
-			const int32_t f = f0 - o, l = l0 - o;
-			if (__builtin_expect(f > -8 || l < (int32_t)PB, 0)) {   // a span edge in this piece
-				const int fc = max(min(f, 24), -8);
-				const int lc = max(min(l, 24), -8);
-				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
-				lo &= byte_mask(fc, lc);
-				hi &= byte_mask(fc - 8, lc - 8);
-				lo ^= byte_mask(fc, fc + 8);   // init = ~0
-				hi ^= byte_mask(fc - 8, fc);
-				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-			}
-			const uint32_t y0 = (uint32_t)A ^ x.x, y1 = (uint32_t)(A >> 32) ^ x.y;
-			uint64_t n = 0;
-			if constexpr (PB == 16) {   // the lookups that do not wait for A
-				n = L(8, x.z & 0xff) ^ L(9, (x.z >> 8) & 0xff) ^ L(10, (x.z >> 16) & 0xff) ^ L(11, x.z >> 24) ^
-				    L(12, x.w & 0xff) ^ L(13, (x.w >> 8) & 0xff) ^ L(14, (x.w >> 16) & 0xff) ^ L(15, x.w >> 24);
-			}
-			A = n ^ L(0, y0 & 0xff) ^ L(1, (y0 >> 8) & 0xff) ^ L(2, (y0 >> 16) & 0xff) ^ L(3, y0 >> 24) ^
-			    L(4, y1 & 0xff) ^ L(5, (y1 >> 8) & 0xff) ^ L(6, (y1 >> 16) & 0xff) ^ L(7, y1 >> 24);
-		}
-	}
-	uint64_t c = A ? gf2_mulmod(A, klane) : 0ull;
-#pragma unroll
-	for (int d = 32; d >= 1; d >>= 1) {
-		const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c, d, 64);
-		const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), d, 64);
-		c ^= ((uint64_t)hi << 32) | lo;
-	}
-	return uni64(c);
-}
-
-// ── five-bit row tables ──
-//
-// The same row fold with the 64-bit (A ^ piece) split into 13 five-bit fields
-// instead of 8 bytes: 13 lookups in tables of 32 entries x 8 B = 256 B, one
-// LDS row across all 64 banks.  A ds_read_b64 is serviced in two 32-lane
-// groups; within a group distinct entries of one table sit on distinct bank
-// pairs and equal entries broadcast, so no lookup ever conflicts (random byte
-// indices into a 2 KiB table cost ~3.5 LDS cycles per group).  13 conflict-free
-// lookups per 8 bytes instead of 8 at ~3.5.  Tables at tb (256-byte aligned),
-// table k at tb + 256 k.
-__device__ __forceinline__ uint64_t fold5(uint32_t lo, uint32_t hi, uint32_t tb) {
-	const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 30);   // bits 30..34
-	auto L = [&](uint32_t k, uint32_t f) -> uint64_t { return ldsq(tb + 256u * k + 8u * f); };
-	return L(0, lo & 31u) ^ L(1, __builtin_amdgcn_ubfe(lo, 5, 5)) ^ L(2, __builtin_amdgcn_ubfe(lo, 10, 5)) ^
-	       L(3, __builtin_amdgcn_ubfe(lo, 15, 5)) ^ L(4, __builtin_amdgcn_ubfe(lo, 20, 5)) ^
-	       L(5, __builtin_amdgcn_ubfe(lo, 25, 5)) ^ L(6, mid & 31u) ^ L(7, __builtin_amdgcn_ubfe(hi, 3, 5)) ^
-	       L(8, __builtin_amdgcn_ubfe(hi, 8, 5)) ^ L(9, __builtin_amdgcn_ubfe(hi, 13, 5)) ^
-	       L(10, __builtin_amdgcn_ubfe(hi, 18, 5)) ^ L(11, __builtin_amdgcn_ubfe(hi, 23, 5)) ^ L(12, hi >> 28);
-}
-
-// crc_seg_rows with the five-bit tables (PB = 8: 13 tables; PB = 16: 26, the
-// second 13 for the piece's high 8 bytes, which do not wait for A).  SEG:
-// segment bytes (64 KiB for the encode passes, 16 KiB in the decode kernel).
-// kCopy (PB = 8): every piece wholly inside [start, copy_hi) is also stored
-// at its address + copy_delta (the decode kernel's in-place image of R, made
-// from the same loads as R's CRC).
-template <uint32_t PB, int kPf, uint32_t SEG = kCrcSegBytes, bool kCopy = false>
-__device__ __forceinline__ uint64_t crc_seg_rows5(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                  uint32_t tb, uint64_t klane, intptr_t copy_delta = 0,
-                                                  uintptr_t copy_hi = 0) {
-	static_assert(!kCopy || PB == 8, "copy: 8-byte pieces");
-	static_assert(PB == 8 || PB == 16, "piece bytes");
-	constexpr uint32_t RB = 64 * PB, NR = SEG / RB;
-	static_assert(NR % kPf == 0, "rows per prefetch batch");
-	const uint32_t lane = lane_id();
-	const uintptr_t end = start + len;
-	const uintptr_t a0 = start & ~(uintptr_t)15;
-	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)nseg * SEG;   // may wrap below a0
-	const uintptr_t p0 = dom + (uintptr_t)j * SEG + (uintptr_t)lane * PB;
-	auto clamp32 = [](intptr_t v) -> int32_t {
-		return (int32_t)(v < -(intptr_t)RB ? -(intptr_t)RB : (v > (intptr_t)(SEG + RB) ? (intptr_t)(SEG + RB) : v));
-	};
-	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)p0);
-	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)p0);
-	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)p0);
-	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-	typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-	typedef __attribute__((address_space(1))) const v4u gv4;
-	typedef __attribute__((address_space(1))) const v2u gv2;
-	// the pieces in flight: 16 B (PB = 16) or 8 B each
-	typedef typename std::conditional<PB == 16, v4u, v2u>::type piece_t;
-	typedef typename std::conditional<PB == 16, gv4, gv2>::type gpiece_t;
-	uint64_t A = 0;
-	for (uint32_t r0 = 0; r0 < NR; r0 += kPf) {
-		piece_t xs[kPf];
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)((r0 + u) * RB);
-			xs[u] = piece_t{};
-			if (o + (int32_t)PB > z0) xs[u] = *reinterpret_cast<gpiece_t*>(p0 + (uintptr_t)(r0 + u) * RB);
-		}
-		if constexpr (kCopy) {
-#pragma unroll
-			for (int u = 0; u < kPf; ++u) {
-				const uintptr_t pa = p0 + (uintptr_t)(r0 + u) * RB;
-				if (pa >= start && pa + PB <= copy_hi)
-					*reinterpret_cast<__attribute__((address_space(1))) v2u*>(pa + copy_delta) = xs[u];
-			}
-		}
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)((r0 + u) * RB);
-			v4u x;
-			if constexpr (PB == 16) x = xs[u];
-			else x = v4u{xs[u].x, xs[u].y, 0u, 0u};
-			const int32_t f = f0 - o, l = l0 - o;
-			if (__builtin_expect(f > -8 || l < (int32_t)PB, 0)) {
-				const int fc = max(min(f, 24), -8);
-				const int lc = max(min(l, 24), -8);
-				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
-				lo &= byte_mask(fc, lc);
-				hi &= byte_mask(fc - 8, lc - 8);
-				lo ^= byte_mask(fc, fc + 8);   // init = ~0
-				hi ^= byte_mask(fc - 8, fc);
-				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-			}
-			uint64_t n = 0;
-			if constexpr (PB == 16) n = fold5(x.z, x.w, tb + 256u * 13u);
-			A = n ^ fold5((uint32_t)A ^ x.x, (uint32_t)(A >> 32) ^ x.y, tb);
-		}
-	}
-	uint64_t c = A ? gf2_mulmod(A, klane) : 0ull;
-#pragma unroll
-	for (int d = 32; d >= 1; d >>= 1) {
-		const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c, d, 64);
-		const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), d, 64);
-		c ^= ((uint64_t)hi << 32) | lo;
-	}
-	return uni64(c);
-}
-
-#ifndef DG_CRC_ROWS
-#define DG_CRC_ROWS 3   // bit 0: the wide pass, bit 1: the pass beside another kernel
-#endif
-
-// Wide: 16-byte pieces, 4 table copies (128 KiB), one 1024-thread block per CU
-// (five-bit tables: 26 x 256 B, conflict-free, no copies).
-__global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
-	extern __shared__ uint64_t TW[];   // 16 tables x 256 x 4 copies
-	if constexpr (DG_CRC5) {
-		for (uint32_t i = threadIdx.x; i < 32 * kCrc5Tabs16; i += kCrcWideBlock) TW[i] = a.tables[kCrc5R16 + i];
-		__syncthreads();
-		const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-		const uint64_t kl = a.tables[kCrcRowK16 + lane];
-		constexpr uint32_t kWaves = kCrcWideBlock / 64;
-		for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
-			const CrcSegDev sd = a.segs[seg];
-			const CrcSpanDev sp = a.spans[sd.span];
-			const uint64_t c = crc_seg_rows5<16, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len,
-			                                                     sp.nseg, sd.j, lds_addr(TW), kl);
-			if (lane == 0) a.seg_crc[seg] = c;
-		}
-		return;
-	}
-	for (uint32_t i = threadIdx.x; i < 16 * 256 * 4; i += kCrcWideBlock) TW[i] = a.tables[kCrcRows16 + (i >> 2)];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-	const uint32_t tb = lds_addr(TW) + 8u * (lane & 3u);
-	const uint32_t tbh = tb + 8u * 2048u * 4u;
-	const uint64_t kl = a.tables[kCrcRowK16 + lane];
-	constexpr uint32_t kWaves = kCrcWideBlock / 64;
-	for (uint32_t seg = blockIdx.x * kWaves + wave; seg < a.n_segs; seg += gridDim.x * kWaves) {
-		const CrcSegDev sd = a.segs[seg];
-		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_rows<16, 4, DG_CRC_WIDE_PF>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len,
-		                                                       sp.nseg, sd.j, tb, tbh, kl);
-		if (lane == 0) a.seg_crc[seg] = c;
-	}
-}
-
-// Beside another kernel: 8-byte pieces, one table copy (16 KiB; five-bit
-// tables: 3.25 KiB).
-__global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
-	if constexpr (DG_CRC5) {
-		__shared__ __attribute__((aligned(256))) uint64_t T5[32 * kCrc5Tabs8];
-		for (uint32_t i = threadIdx.x; i < 32 * kCrc5Tabs8; i += 256) T5[i] = a.tables[kCrc5R8 + i];
-		__syncthreads();
-		const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-		const uint64_t kl = a.tables[kCrcRowK8 + lane];
-		for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs; seg += gridDim.x * kCrcWavesPerBlock) {
-			const CrcSegDev sd = a.segs[seg];
-			const CrcSpanDev sp = a.spans[sd.span];
-			const uint64_t c = crc_seg_rows5<8, 4>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j,
-			                                       lds_addr(T5), kl);
-			if (lane == 0) a.seg_crc[seg] = c;
-		}
-		return;
-	}
-	__shared__ uint64_t T8[8 * 256];
-	for (uint32_t i = threadIdx.x; i < 8 * 256; i += 256) T8[i] = a.tables[kCrcRows8 + i];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
-	const uint32_t tb = lds_addr(T8);
-	const uint64_t kl = a.tables[kCrcRowK8 + lane];
-	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs; seg += gridDim.x * kCrcWavesPerBlock) {
-		const CrcSegDev sd = a.segs[seg];
-		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_rows<8, 1, 8>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j,
-		                                         tb, tb, kl);
-		if (lane == 0) a.seg_crc[seg] = c;
-	}
-}
-
-// segments of seg bytes of a span of len >= 8 bytes at start
-__device__ __forceinline__ uint32_t crc_nseg(uintptr_t start, uint64_t len, uint64_t seg) {
-	const uintptr_t a0 = start & ~(uintptr_t)15, a1 = (start + len + 15) & ~(uintptr_t)15;
-	return (uint32_t)((a1 - a0 + seg - 1) / seg);
-}
-
-// Sized to run beside the onepass kernel (which leaves a CU ~12 KiB of LDS
-// and a SIMD 64 VGPRs): slicing-by-4 tables only (8 KiB LDS), the combine
-// tables read through the cache, at most 64 VGPRs.
+// Sized to run beside the member kernel (which leaves a CU little LDS):
+// slicing-by-4 tables only (8 KiB LDS), the combine tables read through the
+// cache, at most 64 VGPRs.
 __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	__shared__ uint64_t T[4 * 256];
 	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
 	__syncthreads();
 	const uint32_t wave = threadIdx.x >> 6;
-	// grid-stride over the segments (launch_crc may cap the grid: DG_CRC_BLOCKS)
-	for (uint32_t seg = blockIdx.x * kCrcWavesPerBlock + wave; seg < a.n_segs;
+	// grid-stride over the segments (launch_crc may cap the grid)
+	for (uint32_t seg = uni(blockIdx.x * kCrcWavesPerBlock + wave); seg < a.n_segs;
 	     seg += gridDim.x * kCrcWavesPerBlock) {
 		const CrcSegDev sd = a.segs[seg];
 		const CrcSpanDev sp = a.spans[sd.span];
@@ -552,6 +194,54 @@ __global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
 	}
 }
 
+// ── row-interleaved segments (dg_crc.h) ──
+
+// Wide: 16-byte pieces (8 of the 16 lookups per piece do not wait for the
+// register), the 16 tables in 32 KiB, one 1024-thread block per CU: for a CRC
+// pass that has the GPU to itself.  (Four bank-spread table copies, 128 KiB,
+// measured slower: 4.5 vs 4.9 TB/s alone, profiles/r05_crc_lab.txt.)
+constexpr uint32_t kCrcWideBlock = 1024;
+__global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
+	__shared__ __attribute__((aligned(256))) uint64_t TW[16 * 256];
+	for (uint32_t i = threadIdx.x; i < 16 * 256; i += kCrcWideBlock) TW[i] = a.tables[kCrcRows16 + i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+	const uint32_t tb = lds_addr(TW), tbh = tb + 8u * 2048u;
+	const uint64_t kl = a.tables[kCrcRowK16 + lane];
+	constexpr uint32_t kWaves = kCrcWideBlock / 64;
+	for (uint32_t seg = uni(blockIdx.x * kWaves + wave); seg < a.n_segs; seg += gridDim.x * kWaves) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_rows<16, 1, 4>((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, tb,
+		                                          tbh, kl);
+		if (lane == 0) a.seg_crc[seg] = c;
+	}
+}
+
+// Beside another kernel: 8-byte pieces, one table copy (byte tables: 16 KiB;
+// five-bit tables: 3.25 KiB), DG_CRC_PF pieces per lane per batch (two
+// batches in flight), at most 64 VGPRs.
+#ifndef DG_CRC_PF
+#define DG_CRC_PF 2
+#endif
+template <int TAB>
+__global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
+	constexpr uint32_t nt = TAB == kCrcByte ? 8 * 256 : 32 * kCrc5Tabs8;
+	__shared__ __attribute__((aligned(256))) uint64_t T8[nt];
+	for (uint32_t i = threadIdx.x; i < nt; i += 256) T8[i] = a.tables[(TAB == kCrcByte ? kCrcRows8 : kCrc5R8) + i];
+	__syncthreads();
+	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+	const uint32_t tb = lds_addr(T8);
+	const uint64_t kl = a.tables[kCrcRowK8 + lane];
+	for (uint32_t seg = uni(blockIdx.x * kCrcWavesPerBlock + wave); seg < a.n_segs;
+	     seg += gridDim.x * kCrcWavesPerBlock) {
+		const CrcSegDev sd = a.segs[seg];
+		const CrcSpanDev sp = a.spans[sd.span];
+		const uint64_t c = crc_seg_rows<8, 1, DG_CRC_PF, kCrcSegBytes, false, TAB>(
+		    (uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, tb, tb, kl);
+		if (lane == 0) a.seg_crc[seg] = c;
+	}
+}
 
 __global__ __launch_bounds__(64) void crc_finalize_kernel(CrcArgs a) {
 	const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -799,18 +489,14 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
 	if (a.n_segs) {
 		const uint32_t blocks = std::min<uint32_t>(n_cu, (a.n_segs + 15) / 16);
-		if (DG_CRC_ROWS & 1)
-			hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock),
-			                   DG_CRC5 ? 256ull * kCrc5Tabs16 : 8ull * 16 * 256 * 4, st, a);
-		else
-			hipLaunchKernelGGL(crc_segments_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 8ull * 4 * 256 * 16, st, a);
+		hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 0, st, a);
 	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
 	return hipGetLastError();
 }
 
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, bool rows) {
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, int pass) {
 	if (a.n_segs) {
 		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
 		static const uint32_t env_cap = [] {
@@ -819,8 +505,10 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, bo
 		}();
 		const uint32_t cap = env_cap ? env_cap : overlap_cap;
 		if (cap && blocks > cap) blocks = cap;
-		if (rows && (DG_CRC_ROWS & 2))
-			hipLaunchKernelGGL(crc_rows_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+		if (pass == kCrcPassRows)
+			hipLaunchKernelGGL(crc_rows_kernel<kCrcByte>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+		else if (pass == kCrcPassRows5)
+			hipLaunchKernelGGL(crc_rows_kernel<kCrcFive>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 		else
 			hipLaunchKernelGGL(crc_segments_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 	}
@@ -961,8 +649,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 // The block barrier between windows also orders every store of one window
 // before the next window's reads and writes.
 constexpr uint32_t kDecBlock = 256;
-constexpr uint32_t kDecCrcLane = 256;                 // in-kernel CRC: bytes per lane
-constexpr uint64_t kDecCrcSeg = 64ull * kDecCrcLane;  // 16 KiB segments
+constexpr uint32_t kDecCrcSeg = 16384;                // in-kernel CRC: 16 KiB segments
 static_assert(4 * kDecCrcSeg == kCrcSegBytes, "the Horner step (4 segments) is x^(8 kCrcSegBytes)");
 
 // A block barrier that also orders global memory between the block's waves:
@@ -1343,10 +1030,10 @@ __device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uin
 	}
 }
 
-// The decode kernel's CRC segments (DG_DEC_CRC 1: byte-table rows, 2:
-// five-bit rows; 16 KiB segments as rows of 64 x 8 bytes).  The tables go to
-// LDS at tb (256-byte aligned, inside the dead doubling arrays), then the
-// nibble table of x^(8 * 64 KiB) (the Horner step of a wave's segments) at TK.
+// The decode kernel's CRC segments: 16 KiB segments as rows of 64 x 8 bytes
+// (dg_crc.h).  The byte tables go to LDS at tb (256-byte aligned, inside the
+// dead doubling arrays), then the nibble table of x^(8 * 64 KiB) (the Horner
+// step of a wave's segments) at TK.
 struct DecCrc {
 	uint32_t tb;
 	const uint64_t* TK;
@@ -1356,10 +1043,8 @@ __device__ __forceinline__ DecCrc dec_crc_tables(uint16_t* NX, const DecodeArgs&
 	const uint32_t tid = threadIdx.x;
 	const uint32_t base = lds_addr(NX), tb = (base + 255u) & ~255u;
 	uint64_t* T = reinterpret_cast<uint64_t*>(NX) + (tb - base) / 8;
-	constexpr uint32_t nt = DG_DEC_CRC == 2 ? 32 * kCrc5Tabs8 : 8 * 256;
-	const uint32_t src = DG_DEC_CRC == 2 ? kCrc5R8 : kCrcRows8;
-	for (uint32_t k = tid; k < nt; k += kDecBlock) T[k] = a.tables[src + k];
-	uint64_t* TK = T + nt;
+	for (uint32_t k = tid; k < 8 * 256; k += kDecBlock) T[k] = a.tables[kCrcRows8 + k];
+	uint64_t* TK = T + 8 * 256;
 	const uint64_t* KF = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;
 	for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
 	static_assert(8 * (8 * 256 + kCrcNibTabWords) + 256 <= 3 * kDecWin * 2, "CRC tables fit NX");
@@ -1368,10 +1053,7 @@ __device__ __forceinline__ DecCrc dec_crc_tables(uint16_t* NX, const DecodeArgs&
 template <bool kCopy = false>
 __device__ __forceinline__ uint64_t dec_seg_crc(const DecCrc& t, uintptr_t start, uint64_t len, uint32_t nseg,
                                                 uint32_t j, intptr_t copy_delta = 0, uintptr_t copy_hi = 0) {
-	if constexpr (DG_DEC_CRC == 2)
-		return crc_seg_rows5<8, 4, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.klane, copy_delta, copy_hi);
-	else
-		return crc_seg_rows<8, 1, 8, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.tb, t.klane, copy_delta, copy_hi);
+	return crc_seg_rows<8, 1, 8, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.tb, t.klane, copy_delta, copy_hi);
 }
 
 __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void decode_kernel(DecodeArgs a) {
@@ -1455,10 +1137,9 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	// each wave folding its segments Horner-wise; the image's whole 16-byte
 	// words are stored from the same pieces
 	const bool aligned_or = (((uintptr_t)O | (uintptr_t)R) & 15) == 0;
-	const bool rcrc_early = DG_DEC_CRC != 0 && a.crc_check && aligned_or && rl >= 8;
+	const bool rcrc_early = a.crc_check && aligned_or && rl >= 8;
 	uint64_t racc = 0;
 	uint32_t rlast = ~0u;
-#if DG_DEC_CRC
 	if (rcrc_early) {
 		const DecCrc ct = dec_crc_tables(NX, a);
 		__syncthreads();
@@ -1471,7 +1152,6 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		}
 		__syncthreads();   // the tables' LDS is the parse's next
 	}
-#endif
 	{
 		uint64_t k0 = 0;
 		if (aligned_or) {   // 16 B per thread, 4 in flight
@@ -1746,28 +1426,10 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		block_sync_global();   // every wave's output stores before any CRC read
 		const uint64_t* Lv = a.tables + 8 * 256;
 		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
-#if DG_DEC_CRC
 		// LDS (the dead doubling arrays): the row tables and x^(8 * 64 KiB);
 		// 16 KiB segments read as rows of 64 x 8 bytes (coalesced)
 		const DecCrc ct = dec_crc_tables(NX, a);
 		const uint64_t* TK = ct.TK;
-#else
-		// LDS (the dead doubling arrays, 22 of 24 KiB): the slicing-by-4
-		// tables, the tree's levels x^(8 * 256 * 2^l) and x^(8 * 64 KiB)
-		uint64_t* TS = reinterpret_cast<uint64_t*>(NX);
-		uint64_t* TT = TS + 4 * 256;
-		uint64_t* TK = TT + kCrcLevels * kCrcNibTabWords;
-		static_assert(8 * (4 * 256 + (kCrcLevels + 1) * kCrcNibTabWords) <= sizeof(NX), "CRC tables fit NX");
-		for (uint32_t k = tid; k < 4 * 256; k += kDecBlock) TS[k] = a.tables[k];
-		for (uint32_t k = tid; k < (kCrcLevels + 1) * kCrcNibTabWords; k += kDecBlock) {
-			const uint32_t lv = k / kCrcNibTabWords, e = k % kCrcNibTabWords;
-			const uint64_t* src = lv == 0 ? KF + kCrcFinX256 * kCrcNibTabWords
-			                    : lv == 1 ? KF + kCrcFinX512 * kCrcNibTabWords
-			                    : lv < kCrcLevels ? Lv + (lv - 2) * kCrcNibTabWords
-			                                      : KF;   // x^(8 * 64 KiB)
-			TT[k] = src[e];
-		}
-#endif
 		__syncthreads();
 		const uintptr_t sa[2] = {(uintptr_t)R, (uintptr_t)O};
 		const uint64_t sl[2] = {rl, vsize};
@@ -1781,11 +1443,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			} else if (sl[sp] >= 8) {
 				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
 				for (uint32_t j = wave; j < nseg; j += kDecWaves) {
-#if DG_DEC_CRC
 					const uint64_t c = dec_seg_crc(ct, sa[sp], sl[sp], nseg, j);
-#else
-					const uint64_t c = crc_seg_wave<kDecCrcLane>(sa[sp], sl[sp], nseg, j, lds_addr(TS), TT);
-#endif
 					acc = (last != ~0u ? mul_nib(acc, TK) : 0ull) ^ c;   // TK: x^(8 * 64 KiB) = 4 segments
 					last = j;
 				}

@@ -122,3 +122,14 @@ def max_over_ranks(dist, value: float, world: int, device) -> float:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(dist, value: int, world: int, device) -> int:
+    """The job's total of a per-rank count (bytes processed): ranks hold
+    byte-balanced but unequal pair ranges, so rank 0's count times the world
+    size is not the total."""
+    import torch
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())

@@ -276,10 +276,15 @@ int dg_encode_pipelined(dg_context_t *ctx, dg_algorithm_t algo,
  * ranges balanced by sum(|R|+|V|), one host thread per context running
  * dg_encode_pipelined on its range into a private buffer (sized by the
  * range's output bound), then the ranges' deltas are packed into h_out in
- * pair order: h_out, out_offsets and status read exactly as the one-device
- * call leaves them.  No bytes move between devices.  n_ctx == 1 is
- * dg_encode_pipelined.  Returns as dg_encode_pipelined (the first failing
- * range's code when status is NULL). */
+ * pair order: when everything fits, h_out, out_offsets and status read
+ * exactly as the one-device call leaves them.  Under a tight out_cap the
+ * pairs are packed up to the first one that does not fit, and it and every
+ * later pair get DG_ERR_CAPACITY (a pair the device failed keeps its own
+ * status) with out_offsets at the bytes written (the one-device call stops
+ * at a chunk boundary instead).  No bytes move between devices.  n_ctx == 1
+ * is dg_encode_pipelined.  Returns as dg_encode_pipelined (the first failing
+ * range's code when status is NULL).  The multi-device path has only run
+ * with several contexts on one device (tests/test_gpu_pipelined.py). */
 int dg_encode_pipelined_multi(dg_context_t *const *ctxs, uint32_t n_ctx, dg_algorithm_t algo,
                               const uint8_t *h_ref, const uint8_t *h_ver,
                               const dg_pair_t *pairs, uint32_t n_pairs,

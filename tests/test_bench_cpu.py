@@ -35,6 +35,9 @@ def test_bench_launches_n_ranks(gpus):
     rng = d["ranges"]
     assert rng[0][0] == 0 and all(rng[i][1] == rng[i + 1][0] for i in range(gpus - 1))
     assert len({b - a for a, b in rng}) > 1   # the unequal-range case is exercised
+    # value counts the all-reduced sum of every rank's bytes
+    assert d["bytes_job"] == d["bytes_expected"]
+    assert d["bytes_rank0_x_world"] != d["bytes_expected"]
 
 
 def test_bench_rejects_world_mismatch():

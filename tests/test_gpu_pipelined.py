@@ -119,3 +119,47 @@ def test_pipelined_multi_device(dg, orc, n_dev, algo):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_pipelined_multi_tight_capacity(dg, orc):
+    """under a tight out_cap the multi-device call packs the pairs
+    up to the first that does not fit; it and every later pair (also in later
+    ranges with smaller deltas) report DG_ERR_CAPACITY at the bytes written."""
+    import ctypes as C
+    L = dg._lib
+    n = 9
+    # delta sizes differ per pair: pair i's V differs from R in a block of i KiB
+    pairs = []
+    for i in range(n):
+        R = bytes((7 * k + i) & 0xFF for k in range(16384))
+        V = bytearray(R)
+        for k in range(1024 * (i % 4) + 16):
+            V[100 + k] ^= 0x5A
+        pairs.append((R, bytes(V)))
+    want = [orc.encode(ONEPASS, R, V, p=16, q=97) for R, V in pairs]
+    lay = [(i * 16384, 16384, i * 16384, 16384) for i in range(n)]
+    hr = (C.c_uint8 * (n * 16384)).from_buffer_copy(b"".join(R for R, _ in pairs))
+    hv = (C.c_uint8 * (n * 16384)).from_buffer_copy(b"".join(V for _, V in pairs))
+    first = 3   # pairs 0..2 fit, pair 3 (the largest delta) does not; pair 4 alone would
+    cap = sum(len(w) for w in want[:first]) + len(want[first]) - 1
+    ho = (C.c_uint8 * cap)()
+    pa = (L.Pair * n)(*[L.Pair(*x) for x in lay])
+    offs = (C.c_uint64 * (n + 1))(*([12345] * (n + 1)))
+    st = (C.c_int32 * n)(*([0] * n))
+    o = L.DiffOptions.make(q=97)
+    ctxs = [dg.Context(0) for _ in range(3)]
+    try:
+        hs = (C.c_void_p * 3)(*[c.handle for c in ctxs])
+        rc = dg.lib.dg_encode_pipelined_multi(hs, 3, ONEPASS, C.addressof(hr), C.addressof(hv), pa, n, C.byref(o),
+                                              1 << 20, C.addressof(ho), cap, offs, st)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert rc == 7
+    written = sum(len(w) for w in want[:first])
+    assert list(st) == [0] * first + [7] * (n - first)
+    exp = [0]
+    for w in want[:first]:
+        exp.append(exp[-1] + len(w))
+    assert list(offs) == exp + [written] * (n - first)
+    assert bytes(ho[:written]) == b"".join(want[:first])
