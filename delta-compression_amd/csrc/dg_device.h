@@ -13,10 +13,9 @@ constexpr uint64_t kBase = 263;                    // src/c/delta.h:24
 constexpr uint64_t kCrcPoly = 0xC96C5795D7870F42ULL;  // reflected, delta.h:303
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;        // "no slot" (q < 2^32 - 1)
 
-// CRC segmentation: one wave64 per segment, kCrcLaneBytes contiguous bytes per
-// lane.  Segments tile a span from its (16-byte aligned-up) end backwards.
-constexpr uint32_t kCrcLaneBytes = 1024;
-constexpr uint32_t kCrcSegBytes = 64 * kCrcLaneBytes;   // 64 KiB
+// CRC segmentation: one wave64 per 64 KiB segment (dg_crc.h).  Segments tile
+// a span from its (16-byte aligned-up) end backwards.
+constexpr uint32_t kCrcSegBytes = 65536;
 constexpr uint32_t kCrcWavesPerBlock = 4;
 
 // Onepass register history: chunks of 64 steps kept in VGPRs before the
@@ -66,7 +65,9 @@ struct CrcSpanDev {
 
 // Precomputed GF(2) constants for the CRC combine steps, as nibble tables:
 // tab[c][16*j + n] = (n << 4j) * K_c mod P  (reflected), see dg_host.cpp.
-constexpr int kCrcLevels = 6;          // in-wave tree levels
+// Level l = x^(8 * 1024 * 2^l): 16 and 32 KiB are the decode kernel's segment
+// combines, 32 KiB the correcting build's piece stride.
+constexpr int kCrcLevels = 6;
 constexpr int kCrcNibTabWords = 256;   // 16 nibbles x 16 values
 // after the level tables (F): x^(8 kCrcSegBytes), x^(-8t) for t = 0..15,
 // x^(8 kCrcSegBytes k) for k = 2..4, then for the decode kernel's 256-byte
@@ -158,14 +159,6 @@ constexpr uint32_t kSegTail = 0xFFFFFFFFu;
 constexpr uint32_t kMemChunk = 2048;
 constexpr uint32_t kMemAhead = 240;    // staged: [chunk - 16, chunk + 2048 + 240) = 2304 B
 constexpr uint32_t kMemChunkSlots = kMemChunk / 16 + 1;
-// member plans can pipeline the batch in up to kMemGroupsMax groups of
-// consecutive pairs (A/B: DG_MEM_GROUPS).  Off by default: measured C3 440 ->
-// 404 GiB/s and c3s 93 -> 64 (each group's chains become a launch of a
-// quarter of the pairs, and the serialiser's persistent waves hold the CUs
-// the next launches wait for; profiles/r04_experiments.md)
-constexpr uint32_t kMemGroupsMax = 4;
-constexpr uint32_t kMemGroupsDefault = 1;
-
 struct SpecArgs {
 	const uint8_t* ref;
 	const uint8_t* ver;
@@ -198,9 +191,8 @@ struct MemSerArgs {
 	uint8_t* out;
 	uint64_t out_cap;
 	int32_t* status;
-	// sparse deltas: when the whole batch's delta bytes (offsets[n_pairs], the
-	// scan's total) are under 1/8 of sum |V| (v_total), ADD payloads are read
-	// from V in HBM instead of staging every chunk's V bytes; 0 = always stage
+	// sum |V| of the batch: a sparse batch (the scan's total delta bytes,
+	// offsets[n_pairs], under half of it) runs the serialiser's whole grid
 	uint64_t v_total;
 	uint32_t n_pairs;
 };
@@ -290,16 +282,13 @@ hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint3
 hipError_t launch_correcting_clear(const EncodeArgs& a, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
                              hipEvent_t ev_built, hipEvent_t ev_fork);
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st, bool chained = false);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);
-// pass: the row-interleaved pass on byte tables (16 KiB LDS per block), on
-// five-bit tables (3.25 KiB), or the lane-contiguous pass (8 KiB)
-enum : int { kCrcPassRows = 0, kCrcPassRows5 = 1, kCrcPassLanes = 2 };
-#ifndef DG_CRC_MEMBERS
-#define DG_CRC_MEMBERS 2   // the pass beside the member kernel (A/B: make variant)
-#endif
+// pass: the row-interleaved pass on byte tables (16 KiB LDS per block) or on
+// five-bit tables (3.25 KiB: beside the member kernel, which leaves little LDS)
+enum : int { kCrcPassRows = 0, kCrcPassRows5 = 1 };
 hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, int pass = kCrcPassRows);
 // the CRC on 16-byte pieces (32 KiB of tables): for a pass that has the GPU to itself
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st);

@@ -214,7 +214,7 @@ int dg_context_create(int device, dg_context_t** out) {
 			tab[k * 256 + i] = (prev >> 8) ^ tab[prev & 0xff];
 		}
 	for (int lv = 0; lv < kCrcLevels; ++lv) {
-		const uint64_t K = gf2_xpow(8ull * kCrcLaneBytes << lv);
+		const uint64_t K = gf2_xpow(8ull * 1024 << lv);
 		for (int j = 0; j < 16; ++j)
 			for (int nb = 0; nb < 16; ++nb)
 				tab[8 * 256 + lv * kCrcNibTabWords + 16 * j + nb] = gf2_mul(K, (uint64_t)nb << (4 * j));
@@ -419,14 +419,6 @@ struct dg_encode_plan {
 	// fork/join of the CRC kernels onto a side stream
 	hipStream_t side = nullptr;
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-	// member plans: the batch runs as n_groups groups of consecutive pairs;
-	// group g's scan and serialisation (stream ser) overlap the member kernel
-	// of group g + 1 (VALU-bound beside memory-bound)
-	uint32_t n_groups = 1;
-	std::vector<uint32_t> grp_pair, grp_chunk;   // n_groups + 1 boundaries each
-	hipStream_t ser = nullptr;
-	std::vector<hipEvent_t> ev_grp;              // group g's chains done
-	hipEvent_t ev_ser = nullptr;                 // the last group serialised
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
@@ -850,28 +842,6 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		if (!mbad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
 			mbad = 1;
-		// pipeline groups: consecutive pairs, about equal chunk counts; only
-		// for batches big enough that a group still fills the GPU
-		{
-			uint32_t G = kMemGroupsDefault;
-			const char* gg = ab_env("DG_MEM_GROUPS");
-			if (gg) G = std::max<uint32_t>(1u, std::min<uint32_t>(kMemGroupsMax, (uint32_t)strtoul(gg, nullptr, 0)));
-			G = std::min<uint32_t>(G, std::max<uint32_t>(n, 1u));
-			P->grp_pair.assign(1, 0u);
-			P->grp_chunk.assign(1, 0u);
-			for (uint32_t g = 1; g < G; ++g) {
-				const uint64_t want = (uint64_t)P->n_chunks * g / G;
-				uint32_t i = P->grp_pair.back();
-				while (i < n && P->pp[i].chunk_base < want) ++i;
-				if (i > P->grp_pair.back() && i < n) {
-					P->grp_pair.push_back(i);
-					P->grp_chunk.push_back(P->pp[i].chunk_base);
-				}
-			}
-			P->grp_pair.push_back(n);
-			P->grp_chunk.push_back(P->n_chunks);
-			P->n_groups = (uint32_t)P->grp_pair.size() - 1;
-		}
 		if (mbad && ctx->onepass_members != 1) {
 			// automatic mode: member mode is an optimisation, so a batch that
 			// fits with the plain chain still gets a plan
@@ -926,17 +896,6 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			return set_err(ctx, DG_ERR_HIP, "side stream creation failed: %s", hipGetErrorString(e));
 		}
 	}
-	if (P->members && P->n_groups > 1) {
-		e = hipStreamCreateWithFlags(&P->ser, hipStreamNonBlocking);
-		P->ev_grp.assign(P->n_groups, nullptr);
-		for (auto& ev : P->ev_grp)
-			if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice);
-		if (e == hipSuccess) e = hipEventCreateWithFlags(&P->ev_ser, hipEventDisableTiming | hipEventReleaseToDevice);
-		if (e != hipSuccess) {
-			dg_encode_plan_destroy(P);
-			return set_err(ctx, DG_ERR_HIP, "serialiser stream creation failed: %s", hipGetErrorString(e));
-		}
-	}
 	*out = P;
 	return DG_OK;
 }
@@ -971,7 +930,7 @@ const uint32_t* dg_encode_plan_copy_counts_device(const dg_encode_plan_t* P) {
 	return P ? P->d_nrec.as<uint32_t>() : nullptr;
 }
 
-constexpr int kTimingEvents = 8 + 2 * (int)kMemGroupsMax;   // + around each group's member kernel
+constexpr int kTimingEvents = 8;
 constexpr uint32_t kTimingAll = (1u << kTimingEvents) - 1u;
 // the events a run records: all, or around the dominant kernel(s) only —
 // the member kernel (2, 6), the correcting build and scan (2, 7, 3), the
@@ -979,7 +938,7 @@ constexpr uint32_t kTimingAll = (1u << kTimingEvents) - 1u;
 // member kernel: the routed plain chain dominates on data off diagonal 0)
 static uint32_t timing_mask(const dg_encode_plan_t* P) {
 	if (P->timing_mode != DG_TIMING_DOMINANT) return kTimingAll;
-	if (P->members) return (1u << 2) | (1u << 6) | (1u << 3) | (0xFFFFu << 8);   // member kernel(s), then the chains
+	if (P->members) return (1u << 2) | (1u << 6) | (1u << 3);   // the member kernel, then the chains
 	if (P->algo == DG_ALGO_CORRECTING) return (1u << 2) | (1u << 7) | (1u << 3);
 	return (1u << 2) | (1u << 3);
 }
@@ -1034,16 +993,7 @@ int dg_encode_plan_stage_times(dg_encode_plan_t* P, float* ms, const char** name
 		if (hipEventSynchronize(e[last]) != hipSuccess) return 0;
 		for (int i = 0; i < ns; ++i) {
 			float t = 0;
-			if (sel[i] == 5 && P->members && P->n_groups > 1) {
-				// pipelined groups: the member kernels' own time, summed
-				for (uint32_t g = 0; g < P->n_groups; ++g) {
-					float tg = 0;
-					hipEventElapsedTime(&tg, e[8 + 2 * g], e[9 + 2 * g]);
-					t += tg;
-				}
-			} else {
-				hipEventElapsedTime(&t, e[pairs[sel[i]][0]], e[pairs[sel[i]][1]]);
-			}
+			hipEventElapsedTime(&t, e[pairs[sel[i]][0]], e[pairs[sel[i]][1]]);
 			acc[i] += t;
 		}
 	}
@@ -1078,7 +1028,7 @@ static MemSerArgs mem_ser_args(const dg_encode_plan_t* P, const uint8_t* d_ver, 
 	m.out = d_out;
 	m.out_cap = out_cap;
 	m.status = d_status;
-	m.v_total = P->n_groups == 1 ? P->v_total : 0;   // (groups serialise before the scan's total is known)
+	m.v_total = P->v_total;
 	m.n_pairs = P->n;
 	return m;
 }
@@ -1130,15 +1080,16 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		const uint32_t rounds = (P->n + 16u * ctx->n_cu - 1) / (16u * ctx->n_cu);
 		if (!P->skip_crc) {
 			if (P->crc_wide) HIPCHK(ctx, launch_crc_wide(a, ctx->n_cu, cs));
-			// (member plans: the lane-contiguous pass, 8 KiB of LDS.  The byte-table
-			// row pass's 16 KiB blocks find no room beside the member kernel and
-			// trail it; the five-bit row pass (3.25 KiB) finishes sooner but its
-			// VALU slows the member kernel: C3 -2.5 %, c6 +5 %, round 5)
+			// (member plans: the five-bit row pass, 3.25 KiB of LDS: the byte-table
+			// pass's 16 KiB blocks find no room beside the member kernel and trail
+			// it; the member waves run at a higher issue priority, so the pass
+			// takes the VALU slots they leave: C3 +3 %, c6 +10 % over round 4's
+			// lane-contiguous pass, profiles/r05_experiments.md)
 			// (correcting plans: V's CRC runs beside the latency-bound V scan
 			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
 			// there instead of 0.71: C4 731 -> 813 GiB/s)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            P->members ? DG_CRC_MEMBERS : kCrcPassRows));
+			                            P->members ? kCrcPassRows5 : kCrcPassRows));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
@@ -1195,36 +1146,9 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.mem_s = m.mem_s;
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
-				if (P->n_groups == 1) {
-					HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
-					HIPCHK(ctx, rec(6, st));
-					HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
-				} else {
-					// group g: member kernel, chains (run stream); then its scan
-					// and serialisation on the serialiser stream, beside group
-					// g + 1's member kernel
-					MemSerArgs ms = mem_ser_args(P, d_ver, d_out, out_cap, d_offsets, d_status);
-					for (uint32_t g = 0; g < P->n_groups; ++g) {
-						const uint32_t c0 = P->grp_chunk[g], c1 = P->grp_chunk[g + 1];
-						const uint32_t p0 = P->grp_pair[g], p1 = P->grp_pair[g + 1];
-						m.job0 = c0;
-						HIPCHK(ctx, rec(8 + 2 * g, st));
-						HIPCHK(ctx, launch_members(m, c1 - c0, ctx->n_cu, st));
-						HIPCHK(ctx, rec(9 + 2 * g, st));
-						if (g + 1 == P->n_groups) HIPCHK(ctx, rec(6, st));
-						a.pair0 = p0;
-						a.n_pairs = p1;
-						HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
-						HIPCHK(ctx, hipEventRecord(P->ev_grp[g], st));
-						HIPCHK(ctx, hipStreamWaitEvent(P->ser, P->ev_grp[g], 0));
-						HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>() + p0, d_offsets + p0, p1 - p0, P->ser, g > 0));
-						ms.job0 = c0;
-						HIPCHK(ctx, launch_member_serialize(ms, c1 - c0, ctx->n_cu, P->ser));
-					}
-					HIPCHK(ctx, hipEventRecord(P->ev_ser, P->ser));
-					a.pair0 = 0;
-					a.n_pairs = P->n;
-				}
+				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
+				HIPCHK(ctx, rec(6, st));
+				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			} else {
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			}
@@ -1283,15 +1207,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		HIPCHK(ctx, rec(5, st));
 		return DG_OK;
 	}
-	if (P->members && P->n_groups > 1) {
-		// every group already scanned and serialised on the serialiser stream
-		HIPCHK(ctx, rec(4, st));
-		HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_ser, 0));
-		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
-		HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
-		HIPCHK(ctx, rec(5, st));
-		return DG_OK;
-	}
 	// 3. exclusive scan of sizes -> packed offsets
 	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
 	SerArgs s{};
@@ -1329,14 +1244,9 @@ void dg_encode_plan_destroy(dg_encode_plan_t* P) {
 	if (P->side) hipStreamSynchronize(P->side);
 	for (auto& e : P->ev)
 		if (e) hipEventDestroy(e);
-	if (P->ser) hipStreamSynchronize(P->ser);
 	if (P->ev_fork) hipEventDestroy(P->ev_fork);
 	if (P->ev_join) hipEventDestroy(P->ev_join);
-	for (auto& ev : P->ev_grp)
-		if (ev) hipEventDestroy(ev);
-	if (P->ev_ser) hipEventDestroy(P->ev_ser);
 	if (P->side) hipStreamDestroy(P->side);
-	if (P->ser) hipStreamDestroy(P->ser);
 	delete P;
 }
 

@@ -1,6 +1,7 @@
 // dg_kernels.hip — CDNA4 (gfx950) kernels of the delta codec.
 //
-//   crc_segments_kernel / crc_finalize_kernel  CRC-64/XZ of every R and V
+//   crc_rows_kernel / crc_rows_wide_kernel / crc_finalize_kernel  CRC-64/XZ
+//       of every R and V (segment folds in dg_crc.h)
 //       (src/c/delta.h:294-322; main.c:259-260)
 //   onepass_kernel   one wave64 per pair, onepass differencing
 //       (src/c/onepass.c:32-297) in its epoch form
@@ -38,14 +39,10 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
 	return x;
 }
 
-// chained: off[0] already holds the offset this range starts at (the grand
-// total the previous range's scan wrote), else 0
 __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __restrict__ sz,
-                                                          uint64_t* __restrict__ off,
-                                                          uint32_t n, uint32_t chained) {
+                                                          uint64_t* __restrict__ off, uint32_t n) {
 	__shared__ uint64_t wsum[16];
 	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
-	const uint64_t base = chained ? off[0] : 0ull;
 	const uint32_t per = (n + 1023) / 1024;
 	const uint32_t b = tid * per, e = min(b + per, n);
 	uint64_t s = 0;
@@ -56,7 +53,7 @@ __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __rest
 	if (wave == 0) {
 		const uint64_t w = lane < 16 ? wsum[lane] : 0;
 		const uint64_t wi = wave_incl_scan64(w);
-		if (lane < 16) wsum[lane] = base + wi - w;   // exclusive wave offsets
+		if (lane < 16) wsum[lane] = wi - w;   // exclusive wave offsets
 	}
 	__syncthreads();
 	uint64_t run = wsum[wave] + incl - s;
@@ -67,139 +64,23 @@ __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __rest
 	if (tid == 1023) off[n] = wsum[15] + incl;   // the grand total (thread 1023 holds the last run)
 }
 
-// ───────────────────────────── serialisation ──────────────────────────────
-
-__device__ __forceinline__ void put_u32be(uint8_t* o, uint32_t x) {
-	o[0] = (uint8_t)(x >> 24);
-	o[1] = (uint8_t)(x >> 16);
-	o[2] = (uint8_t)(x >> 8);
-	o[3] = (uint8_t)x;
-}
-
-
-
-
 // ───────────────────────────── CRC-64/XZ ──────────────────────────────────
 //
 // Tables (built on the host, uploaded once per context; dg_device.h):
 //   slice[8][256]    slicing-by-8 tables of the reflected polynomial
-//   lvl[6][256]      nibble tables of "multiply by x^(8*L*2^l) mod P",
-//                    L = kCrcLaneBytes, for the lane-contiguous in-wave tree
+//   lvl[6][256]      nibble tables of "multiply by x^(8*1024*2^l) mod P"
 //   the row tables and per-lane constants of dg_crc.h
 // The raw CRC (init 0, no xorout) is linear, leading zero bytes are no-ops
 // and init = ~0 equals XOR-ing 0xFF into the first 8 data bytes, so each
 // segment is hashed from a zero register over a zero-front-padded span and
 // the segments are combined as c_left * x^(8*len_right) ^ c_right.
 
-// ── lane-contiguous segments (member plans: 8 KiB of LDS) ──
-//
-// The raw CRC of segment j (64 LB bytes) by one wave: lane l folds LB
-// contiguous bytes with slicing-by-4 tables in LDS at tb (entry (t, b) at tb
-// + 2048 t + 8 b), then an in-wave tree combines the lanes (level l multiplies
-// by x^(8 LB 2^l): the context's level tables at tree + 256 l).  Each 16-byte
-// load instruction of a wave touches 64 cache lines, the reason the row form
-// (dg_crc.h) is used wherever its 16 KiB of tables fit.
-__device__ __forceinline__ uint64_t slice4_lds(uint64_t crc, uint32_t w, uint32_t tb) {
-	const uint32_t x = (uint32_t)crc ^ w;
-	const uint64_t v[5] = {ldsq(tb + 3 * 2048 + (x & 0xff) * 8), ldsq(tb + 2 * 2048 + ((x >> 8) & 0xff) * 8),
-	                       ldsq(tb + 2048 + ((x >> 16) & 0xff) * 8), ldsq(tb + (x >> 24) * 8), crc >> 32};
-	return xor_tree64<5>(v);
-}
-
-__device__ __forceinline__ uint64_t crc_seg_wave(uintptr_t start, uint64_t len, uint32_t nseg, uint32_t j,
-                                                 uint32_t tb, const uint64_t* tree) {
-	constexpr uint32_t kLaneBytes = kCrcLaneBytes;
-	constexpr uint64_t kSeg = 64ull * kLaneBytes;
-	constexpr int kPf = 4;   // 16-byte loads in flight per lane
-	const uint32_t lane = lane_id();
-	const uintptr_t end = start + len;
-	const uintptr_t a0 = start & ~(uintptr_t)15;
-	const uintptr_t a1 = (end + 15) & ~(uintptr_t)15;
-	const uintptr_t dom = a1 - (uintptr_t)nseg * kSeg;   // may wrap below a0
-	const uintptr_t cs = dom + (uintptr_t)j * kSeg + (uintptr_t)lane * kLaneBytes;
-	uint64_t reg = 0;
-	typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-	typedef __attribute__((address_space(1))) const v4u gcu128;   // global, not flat: loads
-	// count on vmcnt only, so the table reads' lgkmcnt waits do not wait for them
-	// The span's first and last byte relative to the lane's chunk, clamped
-	// to a range that keeps every per-block test in 32-bit arithmetic
-	// (outside [-64, 1024 + 64] they only mean "before" / "after").
-	auto clamp32 = [](intptr_t v) -> int32_t {
-		return (int32_t)(v < -64 ? -64 : (v > (intptr_t)kLaneBytes + 64 ? (intptr_t)kLaneBytes + 64 : v));
-	};
-	const int32_t f0 = clamp32((intptr_t)start - (intptr_t)cs);   // first data byte
-	const int32_t l0 = clamp32((intptr_t)end - (intptr_t)cs);     // one past the last
-	const int32_t z0 = clamp32((intptr_t)a0 - (intptr_t)cs);      // first 16-byte word with data
-	for (uint32_t w0 = 0; w0 < kLaneBytes; w0 += 16 * kPf) {
-		v4u xs[kPf];
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)(w0 + 16 * u);
-			// words wholly before the data are virtual zeros: no-ops on a zero register
-			xs[u] = v4u{0, 0, 0, 0};
-			if (o + 16 > z0) xs[u] = *reinterpret_cast<gcu128*>(cs + w0 + 16 * u);
-		}
-#pragma unroll
-		for (int u = 0; u < kPf; ++u) {
-			const int32_t o = (int32_t)(w0 + 16 * u);
-			v4u x = xs[u];
-			const int32_t f = f0 - o;   // first data byte index in this word
-			const int32_t l = l0 - o;   // one past last
-			if (__builtin_expect(f > -8 || l < 16, 0)) {   // only the span's edges need masking
-				const int fc = max(min(f, 24), -8);
-				const int lc = max(min(l, 24), -8);
-				uint64_t lo = ((uint64_t)x.y << 32) | x.x, hi = ((uint64_t)x.w << 32) | x.z;
-				lo &= byte_mask(fc, lc);
-				hi &= byte_mask(fc - 8, lc - 8);
-				// init = ~0: invert the span's first 8 bytes
-				lo ^= byte_mask(fc, fc + 8);
-				hi ^= byte_mask(fc - 8, fc);
-				x = v4u{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-			}
-			reg = slice4_lds(reg, x.x, tb);
-			reg = slice4_lds(reg, x.y, tb);
-			reg = slice4_lds(reg, x.z, tb);
-			reg = slice4_lds(reg, x.w, tb);
-		}
-	}
-	// in-wave tree: combine(left, right) = left * x^(8*len(right)) ^ right
-#pragma unroll
-	for (int lv = 0; lv < kCrcLevels; ++lv) {
-		const int d = 1 << lv;
-		const uint32_t plo = (uint32_t)__shfl_down((int)(uint32_t)reg, d, 64);
-		const uint32_t phi = (uint32_t)__shfl_down((int)(uint32_t)(reg >> 32), d, 64);
-		const uint64_t right = ((uint64_t)phi << 32) | plo;
-		const uint64_t shifted = mul_nib(reg, tree + lv * kCrcNibTabWords);
-		if ((lane & (2 * d - 1)) == 0) reg = shifted ^ right;
-	}
-	return uni64(reg);
-}
-
-// Sized to run beside the member kernel (which leaves a CU little LDS):
-// slicing-by-4 tables only (8 KiB LDS), the combine tables read through the
-// cache, at most 64 VGPRs.
-__global__ __launch_bounds__(256, 8) void crc_segments_kernel(CrcArgs a) {
-	__shared__ uint64_t T[4 * 256];
-	for (uint32_t i = threadIdx.x; i < 4 * 256; i += 256) T[i] = a.tables[i];
-	__syncthreads();
-	const uint32_t wave = threadIdx.x >> 6;
-	// grid-stride over the segments (launch_crc may cap the grid)
-	for (uint32_t seg = uni(blockIdx.x * kCrcWavesPerBlock + wave); seg < a.n_segs;
-	     seg += gridDim.x * kCrcWavesPerBlock) {
-		const CrcSegDev sd = a.segs[seg];
-		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_wave((uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, lds_addr(T),
-		                                a.tables + 8 * 256);
-		if (lane_id() == 0) a.seg_crc[seg] = c;
-	}
-}
-
 // ── row-interleaved segments (dg_crc.h) ──
 
 // Wide: 16-byte pieces (8 of the 16 lookups per piece do not wait for the
 // register), the 16 tables in 32 KiB, one 1024-thread block per CU: for a CRC
 // pass that has the GPU to itself.  (Four bank-spread table copies, 128 KiB,
-// measured slower: 4.5 vs 4.9 TB/s alone, profiles/r05_crc_lab.txt.)
+// measured slower: 4.8 vs 5.1 TB/s alone, profiles/r05_crc_lab_product.txt.)
 constexpr uint32_t kCrcWideBlock = 1024;
 __global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
 	__shared__ __attribute__((aligned(256))) uint64_t TW[16 * 256];
@@ -471,8 +352,8 @@ hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_
 	return hipGetLastError();
 }
 
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st, bool chained) {
-	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n, chained ? 1u : 0u);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
+	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
 	return hipGetLastError();
 }
 
@@ -505,12 +386,10 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, in
 		}();
 		const uint32_t cap = env_cap ? env_cap : overlap_cap;
 		if (cap && blocks > cap) blocks = cap;
-		if (pass == kCrcPassRows)
-			hipLaunchKernelGGL(crc_rows_kernel<kCrcByte>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
-		else if (pass == kCrcPassRows5)
+		if (pass == kCrcPassRows5)
 			hipLaunchKernelGGL(crc_rows_kernel<kCrcFive>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 		else
-			hipLaunchKernelGGL(crc_segments_kernel, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+			hipLaunchKernelGGL(crc_rows_kernel<kCrcByte>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);

@@ -697,6 +697,11 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 // of LDS: 5 waves per SIMD to hide the LDS and DMA latencies of the rounds.
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_MEM_WAVES, 8))) void member_chunk_kernel(SpecArgs a, uint32_t n_chunks) {
+	// The member waves issue ahead of the CRC pass's waves sharing their SIMDs
+	// (the five-bit CRC rows take the VALU slots they leave): C3 444 -> 458,
+	// c6 1177 -> 1287 GiB/s; with the lane-contiguous CRC pass the CRC starved
+	// (profiles/r05_experiments.md)
+	__builtin_amdgcn_s_setprio(1);
 	__shared__ __attribute__((aligned(16))) ChunkLds L;
 	const uint32_t lane = lane_id();
 	JobCursor J;
@@ -799,10 +804,6 @@ constexpr uint32_t kSerWavesPerCu = DG_MSER_WAVES;   // persistent serialiser wa
 #define DG_MSER_WAVES_SPARSE 24
 #endif
 constexpr uint32_t kSerWavesSparse = DG_MSER_WAVES_SPARSE;   // ... for a sparse batch (delta < |V| / 2)
-#ifndef DG_MSER_DIRECT_DIV
-#define DG_MSER_DIRECT_DIV 8
-#endif
-constexpr uint64_t kSerDirectDiv = DG_MSER_DIRECT_DIV;   // ADD payloads read from V when delta < |V| / this
 
 // one job's inputs, loaded a job ahead (descriptors wave-uniform)
 struct SerFetch {
@@ -816,7 +817,7 @@ struct SerFetch {
 
 // every load unconditional (no branch for the compiler to drain before the
 // loads of the job after it are issued)
-__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F, bool direct) {
+__device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F) {
 	const uint32_t lane = lane_id();
 	const JobCursor& J = F.J;
 	F.st = a.status[J.pair];
@@ -828,10 +829,8 @@ __device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F, bool
 	F.slot0 = J.mem_base + (uint64_t)J.c * kMemChunkSlots;
 	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
 	const uint8_t* V = a.ver + J.v_off;
-	if (!direct) {
 #pragma unroll
-		for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
-	}
+	for (uint32_t k = 0; k < kStageRows; ++k) F.v[k] = load16_async(V, g0 + 1024 * k + 16 * lane, J.vl);
 	F.r = make_uint4(0u, 0u, 0u, 0u);   // (slots 0..63 of the chunk's 129, only the bulk members')
 	if (lane < F.cnt) F.r = *(const uint4*)(a.srec + 4ull * (F.slot0 + lane));
 	F.first = a.mem_s[F.slot0];
@@ -843,18 +842,19 @@ __device__ __forceinline__ void ser_fetch(const MemSerArgs& a, SerFetch& F, bool
 // segments 2c, 2c + 1 (record runs of the chain's own epochs, the tail), so
 // all the chunks of a pair serialise at once.  Persistent waves over
 // contiguous jobs, each job's inputs loaded while the previous one is written.
-template <bool direct>
+// (ADD payloads read straight from V instead of the staged chunk measured
+// slower even on the sparsest bench batch, c6: profiles/r04_experiments.md.)
 __device__ __forceinline__ void member_serialize(const MemSerArgs& a, uint32_t j0, uint32_t j1, uint8_t* vbuf,
                                                  uint8_t* stage) {
 	const uint32_t lane = lane_id();
 	SerFetch F, N;
 	F.J.start(a, j0);
-	ser_fetch(a, F, direct);
+	ser_fetch(a, F);
 	for (uint32_t j = j0; j < j1; ++j) {
 		if (j + 1 < j1) {
 			N.J = F.J;
 			N.J.next(a);
-			ser_fetch(a, N, direct);
+			ser_fetch(a, N);
 		}
 		const uint32_t vl = F.J.vl;
 		const uint8_t* V = a.ver + F.J.v_off;
@@ -865,22 +865,15 @@ __device__ __forceinline__ void member_serialize(const MemSerArgs& a, uint32_t j
 				uint8_t* out = a.out + F.base;
 				if (F.J.c == 0) put_header(out, vl);
 				if (F.cnt) {
-					// ADD payloads from the chunk's V bytes staged in LDS, or
-					// (sparse deltas) straight from V: every payload is followed
-					// by a COPY of >= 16 bytes, so its <= 3-byte spill reads stay in V
-					int64_t g0 = (int64_t)F.J.c * kMemChunk - 16;
+					// ADD payloads from the chunk's V bytes staged in LDS
+					const int64_t g0 = (int64_t)F.J.c * kMemChunk - 16;
 					const uint8_t* vb = vbuf;
-					if (direct) {
-						g0 = 0;
-						vb = V;
-					} else {
-						lds_order();
+					lds_order();
 #pragma unroll
-						for (uint32_t k = 0; k < kStageRows; ++k)
-							if (1024 * k + 16 * lane < kStage)
-								*(uint4*)(vbuf + 1024 * k + 16 * lane) = stage_piece(F.v[k], V, g0 + 1024 * k + 16 * lane, vl);
-						lds_order();
-					}
+					for (uint32_t k = 0; k < kStageRows; ++k)
+						if (1024 * k + 16 * lane < kStage)
+							*(uint4*)(vbuf + 1024 * k + 16 * lane) = stage_piece(F.v[k], V, g0 + 1024 * k + 16 * lane, vl);
+					lds_order();
 					uint64_t pos = F.boff;
 					uint32_t prev_end = F.first;
 					for (uint32_t t0 = 0; t0 < F.cnt; t0 += 64) {
@@ -953,14 +946,12 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
 	// (uniform for the launch: the scan's total is final before this kernel)
 	const uint64_t dtot = a.v_total ? uni64(a.offsets[a.n_pairs]) : ~0ull;
-	const bool direct = dtot * kSerDirectDiv < a.v_total;
 	const uint32_t grid = dtot * 2 < a.v_total ? gridDim.x : umin32(gridDim.x, staged_grid);
 	if (blockIdx.x >= grid) return;
 	const uint32_t j0 = a.job0 + (uint32_t)((uint64_t)n_jobs * blockIdx.x / grid);
 	const uint32_t j1 = a.job0 + (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / grid);
 	if (j0 >= j1) return;
-	if (direct) member_serialize<true>(a, j0, j1, vbuf, stage);
-	else member_serialize<false>(a, j0, j1, vbuf, stage);
+	member_serialize(a, j0, j1, vbuf, stage);
 }
 
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {

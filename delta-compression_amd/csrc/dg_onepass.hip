@@ -176,7 +176,6 @@ struct GlobalSrc {
 	uint32_t p;
 	const uint64_t* powc;
 	__device__ void chunk(uint32_t, uint32_t, bool, bool) {}
-	__device__ void drop_list() {}
 	__device__ uint64_t fpV(uint32_t pos) { return window_fp<PF>(V + pos, p, powc); }
 	__device__ uint64_t fpR(uint32_t pos) { return window_fp<PF>(R + pos, p, powc); }
 	__device__ uint32_t extend(uint32_t vpos, uint32_t rpos, uint32_t lim) {
@@ -200,19 +199,7 @@ constexpr uint32_t kLook = DG_LOOK_BYTES;   // diagonal batch: lookahead bytes p
 #endif
 constexpr uint32_t kShortT = DG_SHORT_T;    // look-back by DPP shifts up to this epoch length
 constexpr uint32_t kWinStride = kWin + 16;  // + slack for the 2nd dword of rd4
-constexpr uint32_t kListCap = 128;          // cached mismatch-list entries (u16, LDS)
-#ifndef DG_LIST_REUSE
-#define DG_LIST_REUSE 16
-#endif
-#ifndef DG_LIST_CACHE
-#define DG_LIST_CACHE 0   // A/B: +2.5% at C3, -6% at C2 (code layout), off
-#endif
-constexpr bool kListCache = DG_LIST_CACHE;
-#ifndef DG_LIST_MIN_CACHE
-#define DG_LIST_MIN_CACHE 1
-#endif
-constexpr uint32_t kListMinCache = DG_LIST_MIN_CACHE;   // only lists this long are looked up again
-constexpr uint32_t kListReuse = DG_LIST_REUSE;   // reuse a cached list with at least this many entries left
+constexpr uint32_t kListCap = 128;          // mismatch-list entries of a diagonal batch (u16, LDS)
 #ifndef DG_BLOOM_BASE
 #define DG_BLOOM_BASE 48
 #endif
@@ -233,15 +220,11 @@ struct WinSrc {
 	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
 	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
 	const uint64_t* powc;
-	// Mismatch list of the diagonal batch, kept across calls (LDS, u16
-	// offsets from lc_base, ascending; the stream end counts as one): the
-	// next call usually starts on one of its entries, so the 2 KiB mask
-	// scan runs once per list instead of once per call.
+	// Mismatch list of the diagonal batch (LDS, u16 offsets from lc_base,
+	// ascending; the stream end counts as one), made afresh by every call.
+	// (Keeping it across calls measured +2.5 % at C3, -6 % at C2: removed.)
 	uint16_t* lc;            // kListCap entries
-	uint32_t lc_base = 0, lc_diag = 0, lc_n = 0;
-	bool lc_end = false;     // the list ends with the stream-end entry
-	// phase C reuses lc's LDS for its per-chunk bitmaps: the list is gone
-	__device__ void drop_list() { lc_n = 0; }
+	uint32_t lc_base = 0, lc_n = 0;
 	PROF_DECL
 #ifdef DG_REFILL_PROF
 	uint64_t refill_cycles = 0;
@@ -383,85 +366,59 @@ struct WinSrc {
 		const uint32_t lim = umin32(vl - v0, rl - r0);
 		if (lim < p + 1) return DiagOut{0, 0, 0, 0, 0};
 		[[maybe_unused]] uint64_t tq = PROF_NOW();
-		// 1. the list of mismatch offsets: entries i0.. of the cached list when
-		//    (v0, r0) is one of them on the same diagonal and enough remain,
-		//    else a new list from v0
-		uint32_t i0 = 0xFFFFFFFFu;
-		if (kListCache && lc_n >= kListMinCache && v0 - r0 == lc_diag && v0 >= lc_base && v0 - lc_base < 65535u) {
-			const uint32_t rel = v0 - lc_base;
-			for (uint32_t c = 0; c < lc_n; c += 64) {
-				const uint32_t e = c + lane < lc_n ? (uint32_t)lc[c + lane] : 0xFFFFFFFFu;
-				const uint64_t m = __ballot(e == rel);
-				if (m) { i0 = c + ffs64(m); break; }
-				if (!__ballot(e < rel)) break;
+		// 1. the list of mismatch offsets from v0
+		ensure2(v0, r0, 64 * kLook + 48, true, true);
+		{
+			// mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
+			const uint32_t base = kLook * lane;
+			// The lane's 32 bytes of each stream come in as three ds_read_b128 from
+			// the 16-byte-aligned address below them (2-way bank conflicts; word
+			// reads at a 32-byte lane stride are 8-way).  The offset inside the
+			// 16 bytes is wave-uniform (windows and lane chunks are 16-aligned),
+			// so picking the 8 words is a uniform switch plus alignbytes.
+			static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
+			uint32_t wv[8], wr[8];
+			lane_words32(0, v0 + base, wv);
+			lane_words32(1, r0 + base, wr);
+			// byte j of word g first lands at bit 8j + g (one shift-and-or per
+			// word), then a 5-bit index rotation (four delta swaps) moves it to
+			// bit 4g + j, i.e. offset order
+			uint32_t bits = 0;
+#pragma unroll
+			for (uint32_t g = 0; g < 8; ++g) {
+				const uint32_t x = wv[g] ^ wr[g];
+				const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
+				bits |= (t >> (7 - g)) & (0x01010101u << g);
 			}
-			if (i0 != 0xFFFFFFFFu && lc_n - i0 < kListReuse && !lc_end) i0 = 0xFFFFFFFFu;
+			bits = mask_transpose_8x4(bits);
+			if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
+				bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
+				if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
+			}
+			// ordered list (exclusive prefix of counts), at most kListCap entries
+			const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+			const uint32_t incl = wave_incl_scan(cnt);
+			uint32_t pos = incl - cnt;
+			const uint32_t total = rdlane(incl, 63);
+			for (uint32_t b = bits; b && pos < kListCap; b &= b - 1, ++pos) lc[pos] = (uint16_t)(base + __builtin_ctz(b));
+			lc_n = umin32(total, kListCap);
+			lc_base = v0;
+			__builtin_amdgcn_s_waitcnt(0xc07f);
+			__builtin_amdgcn_wave_barrier();
 		}
-		uint32_t K, rel0, ak, an;
-		bool gap, fresh = false;
-		uint64_t G;
-		for (;;) {
-			if (i0 == 0xFFFFFFFFu) {
-				ensure2(v0, r0, 64 * kLook + 48, true, true);
-				// mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
-				const uint32_t base = kLook * lane;
-				// The lane's 32 bytes of each stream come in as three ds_read_b128 from
-				// the 16-byte-aligned address below them (2-way bank conflicts; word
-				// reads at a 32-byte lane stride are 8-way).  The offset inside the
-				// 16 bytes is wave-uniform (windows and lane chunks are 16-aligned),
-				// so picking the 8 words is a uniform switch plus alignbytes.
-				static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
-				uint32_t wv[8], wr[8];
-				lane_words32(0, v0 + base, wv);
-				lane_words32(1, r0 + base, wr);
-				// byte j of word g first lands at bit 8j + g (one shift-and-or per
-				// word), then a 5-bit index rotation (four delta swaps) moves it to
-				// bit 4g + j, i.e. offset order
-				uint32_t bits = 0;
-	#pragma unroll
-				for (uint32_t g = 0; g < 8; ++g) {
-					const uint32_t x = wv[g] ^ wr[g];
-					const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;   // bit 8j+7: byte j != 0
-					bits |= (t >> (7 - g)) & (0x01010101u << g);
-				}
-				bits = mask_transpose_8x4(bits);
-				if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
-					bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
-					if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
-				}
-				// ordered list (exclusive prefix of counts), at most kListCap entries
-				const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
-				const uint32_t incl = wave_incl_scan(cnt);
-				uint32_t pos = incl - cnt;
-				const uint32_t total = rdlane(incl, 63);
-				for (uint32_t b = bits; b && pos < kListCap; b &= b - 1, ++pos) lc[pos] = (uint16_t)(base + __builtin_ctz(b));
-				lc_n = umin32(total, kListCap);
-				lc_end = lim <= 64 * kLook && total <= kListCap;
-				lc_base = v0;
-				lc_diag = v0 - r0;
-				i0 = 0;
-				fresh = true;
-				__builtin_amdgcn_s_waitcnt(0xc07f);
-				__builtin_amdgcn_wave_barrier();
-			}
-			K = umin32(lc_n - i0, 64u);
-			if (K < 2) return DiagOut{0, 0, 0, 0, 0};
-			rel0 = v0 - lc_base;
-			{
-				// the window must hold every byte the batch's steps read
-				const uint32_t last = (uint32_t)lc[i0 + K - 1] - rel0;
-				ensure2(v0, r0, last + 16 + 8, true, true);
-			}
-			PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
-			tq = PROF_NOW();
-			ak = lane < K ? (uint32_t)lc[i0 + lane] - rel0 : 0xFFFFFFFFu;
-			an = lane + 1 < K ? (uint32_t)lc[i0 + lane + 1] - rel0 : 0xFFFFFFFFu;
-			gap = lane + 1 < K && an - ak > p;   // a long gap follows a_lane
-			G = __ballot(gap);
-			// a cached tail that closes no member: list afresh from v0 instead
-			if (G == 0 && !fresh && !lc_end) { i0 = 0xFFFFFFFFu; continue; }
-			break;
+		const uint32_t K = umin32(lc_n, 64u);
+		if (K < 2) return DiagOut{0, 0, 0, 0, 0};
+		{
+			// the window must hold every byte the batch's steps read
+			const uint32_t last = (uint32_t)lc[K - 1];
+			ensure2(v0, r0, last + 16 + 8, true, true);
 		}
+		PROF_ADD(*this, P_T_D1, PROF_NOW() - tq);
+		tq = PROF_NOW();
+		const uint32_t ak = lane < K ? (uint32_t)lc[lane] : 0xFFFFFFFFu;
+		const uint32_t an = lane + 1 < K ? (uint32_t)lc[lane + 1] : 0xFFFFFFFFu;
+		const bool gap = lane + 1 < K && an - ak > p;   // a long gap follows a_lane
+		const uint64_t G = __ballot(gap);
 		// 3. the chain of epochs.  From a_0 the chain visits exactly the
 		//    mismatches that follow a long gap: member r starts right after
 		//    the (r-1)-th long gap and ends (first equal step) at the r-th,
@@ -469,7 +426,7 @@ struct WinSrc {
 		//    order, T + 1 steps each, while they fit in 64 lanes and T < 64.
 		const uint64_t gbelow = G & ((1ull << lane) - 1ull);
 		const uint32_t sidx = gbelow ? 64u - (uint32_t)__builtin_clzll(gbelow) : 0u;
-		const uint32_t astart = (uint32_t)lc[i0 + sidx] - rel0;   // sidx <= lane < K
+		const uint32_t astart = (uint32_t)lc[sidx];   // sidx <= lane < K
 		const uint32_t T = gap ? ak + 1 - astart : 0u;
 		const uint64_t tooLong = __ballot(gap && T > 63);
 		const uint32_t kb = tooLong ? ffs64(tooLong) : 64u;
@@ -1090,7 +1047,6 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 				[[maybe_unused]] const uint64_t tc0 = PROF_NOW();
 				if (!in_table) {
 					in_table = true;
-					src.drop_list();
 					if (tslot < 0) {
 						// Holders never wait (a table is released when its pair
 						// ends), so the wait always drains; the wall-clock bound

@@ -74,8 +74,9 @@ def torch_cuda():
 def ctx_mode(dg, request):
     """A context per onepass chain mode (DG_LIMIT_ONEPASS_MEMBERS): verified
     diagonal members first, the plain per-pair chain, or the automatic choice
-    (members for large pairs; pairs whose matches leave diagonal 0 routed to
-    the segment chains, dg_onepass.hip)."""
+    (members for large pairs; pairs whose chunks verify fewer than 2 members
+    each on average, i.e. whose matches leave diagonal 0, routed to the plain
+    per-pair chain after the member chain, dg_onepass.hip)."""
     c = dg.Context(0)
     c.set_limit(dg.LIMIT_ONEPASS_MEMBERS, {"members": dg.MEMBERS_ON, "chain": dg.MEMBERS_OFF,
                                            "auto": dg.MEMBERS_AUTO}[request.param])
