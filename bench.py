@@ -123,20 +123,37 @@ def load_shard():
     return mod
 
 
+def lib_sha16():
+    """The product library's identity (sha256 of the .so, 16 hex digits): a
+    PMC traffic summary is only reported for the library it was measured on."""
+    import hashlib
+    path = os.path.join(PKG_DIR, "lib", "libdeltagpu.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_traffic(config, kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (scripts/pmc_traffic.sh -> profiles/<round>_pmc_traffic_<config>.json:
-    FETCH_SIZE/WRITE_SIZE passes, gfx950 corrections applied), or None."""
+    (scripts/profile_round.sh + profile_collect.py -> profiles/<round>_pmc_traffic_
+    <config>.json: FETCH_SIZE/WRITE_SIZE passes, gfx950 corrections applied),
+    or None.  A summary measured on another build of the library is stale (a
+    kernel change moves the traffic) and is not reported: the source says so."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_traffic_{config}.json")))
+    cur = lib_sha16()
+    stale = None
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
         if d.get("kernel") == kernel and d.get("hbm_bytes_per_launch"):
-            return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
-    return None, None
+            if d.get("lib_sha16") and d["lib_sha16"] == cur:
+                return int(d["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+            stale = stale or os.path.relpath(f, ROOT)
+    return None, (f"stale: {stale} was measured on another build of the library" if stale else None)
 
 
 # ───────────────────────────── CPU baseline ─────────────────────────────────
@@ -472,6 +489,7 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "path_frac": round(path_bytes / step_s / 1e9 / HBM_PEAK_GBS, 5),
         },
         "cpu_baseline": None,
+        "lib_sha16": lib_sha16(),
     }
     if algo == "correcting" and stages.get("corr_build") is not None:
         # the build and the scan apart (HIP events on the run stream; the
@@ -604,6 +622,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
                      "path_achieved": round(alg / step_s / 1e9, 2),
                      "path_frac": round(alg / step_s / 1e9 / HBM_PEAK_GBS, 5)},
         "cpu_baseline": None,
+        "lib_sha16": lib_sha16(),
     }
     yield line
     plan.close()
@@ -741,6 +760,8 @@ def _roof_short(r):
     out = {k: r[k] for k in keys if k in r}
     if r.get("traffic") and r.get("algorithmic_bytes_per_launch"):
         out["traffic_ratio"] = round(r["traffic"] / r["algorithmic_bytes_per_launch"], 3)
+    if r.get("traffic") is None and str(r.get("traffic_source") or "").startswith("stale"):
+        out["traffic_stale"] = True   # the committed PMC summary is of another library build
     return out
 
 
@@ -770,7 +791,7 @@ def compact_line(line, also, full_path):
     with roofline and cpu_baseline, `also` one short object per config,
     at most LINE_MAX bytes; every other field is in `full_path`."""
     keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "untimed_steps", "ms_per_step",
-            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "lib_sha16")
     out = {k: line[k] for k in keep if k in line}
     cfg = line["config"]
     out["config"] = {k: cfg[k] for k in ("workload", "name", "algorithm", "pairs_per_gpu", "pairs_total",

@@ -126,7 +126,8 @@ def main():
         f, nf = counter(d, "FETCH_SIZE")
         w, nw = counter(os.path.join(src, f"pmc_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
         bj = os.path.join(src, f"pmc_{cfg}_FETCH_SIZE.json")
-        kname = json.load(open(bj))["roofline"]["kernel"] if os.path.exists(bj) else None
+        bline = json.load(open(bj)) if os.path.exists(bj) else {}
+        kname = bline.get("roofline", {}).get("kernel")
         raw_f = sum(f.values()) * 1024
         raw_w = sum(w.values()) * 1024
         cls = FETCH_CLASS.get(kname, "dma16")
@@ -138,7 +139,8 @@ def main():
         table_tier = cfg in ("c3s", "c3s_chain", "c4o", "c4o_chain")
         if table_tier:
             cls, fac = "mixed: LDS-DMA windows + random 16-byte table loads", 1.0
-        res = {"kernel": kname, "config": cfg, "kernels": {k: {"fetch_kib": f.get(k), "write_kib": w.get(k),
+        res = {"kernel": kname, "config": cfg, "lib_sha16": bline.get("lib_sha16"),
+               "kernels": {k: {"fetch_kib": f.get(k), "write_kib": w.get(k),
                                                                  "dispatches": [nf.get(k), nw.get(k)]}
                                                              for k in sorted(set(f) | set(w))},
                "fetch_bytes_raw": raw_f, "write_bytes": raw_w,
