@@ -289,7 +289,9 @@ hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_
 // pass: the row-interleaved pass on byte tables (16 KiB LDS per block) or on
 // five-bit tables (3.25 KiB: beside the member kernel, which leaves little LDS)
 enum : int { kCrcPassRows = 0, kCrcPassRows5 = 1 };
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, int pass = kCrcPassRows);
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap = 0, int pass = kCrcPassRows,
+                      bool finalize = true);
+hipError_t launch_crc_finalize(const CrcArgs& a, hipStream_t st);   // the per-span combine alone
 // the CRC on 16-byte pieces (32 KiB of tables): for a pass that has the GPU to itself
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t st);

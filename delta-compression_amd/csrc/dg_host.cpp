@@ -5,6 +5,7 @@
 // dg_kernels.hip on one HIP stream, and moves host buffers through pinned
 // staging for the host-memory entry points.  There is no CPU compute
 // fallback: without a GPU every entry point fails with DG_ERR_NO_DEVICE.
+#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -421,6 +422,8 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
+	int crc_join = 2;          // member plans: 2 = the CRC's combine after the chains, 1 = the chains
+	                           // wait for the whole CRC, 0 = neither (DG_CRC_JOIN, A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
@@ -882,6 +885,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = ab_env("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
+	const char* cj = ab_env("DG_CRC_JOIN");
+	if (cj) P->crc_join = (int)strtol(cj, nullptr, 0);
 	const char* sk = ab_env("DG_SKIP_CRC");
 	P->skip_crc = sk && sk[0] == '1';
 
@@ -1060,8 +1065,12 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		if (!P->timing || !(timing_mask(P) & (1u << k))) return hipSuccess;
 		return hipEventRecord(P->cur[k], s);
 	};
-	auto run_crc = [&]() -> int {
-		HIPCHK(ctx, rec(0, cs));
+	// member plans: the per-span combine (crc_finalize) waits on the run
+	// stream for the chains.  Enqueued right after the row pass, its waves
+	// queue behind the chains' full grid and slowed the routed chain of c3s
+	// by 13 % (40.9 vs 36.2 ms, profiles/r05_experiments.md).
+	const bool late_fin = P->members && P->crc_join == 2 && !serial && !P->crc_wide && !P->fused;
+	auto crc_args = [&]() {
 		CrcArgs a{};
 		a.arena[0] = d_ref;
 		a.arena[1] = d_ver;
@@ -1074,6 +1083,11 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
+		return a;
+	};
+	auto run_crc = [&]() -> int {
+		HIPCHK(ctx, rec(0, cs));
+		const CrcArgs a = crc_args();
 		// beside the differencing: 2 blocks per CU per round of differencing
 		// waves (16 per CU), so the CRC neither crowds one round out nor
 		// trails a multi-round batch (C2: 4096 pairs -> 512 blocks)
@@ -1089,13 +1103,14 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
 			// there instead of 0.71: C4 731 -> 813 GiB/s)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            P->members ? kCrcPassRows5 : kCrcPassRows));
+			                            P->members ? kCrcPassRows5 : kCrcPassRows, !late_fin));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
 	};
 	// differencing -> COPY records + per-pair delta sizes
-	auto run_diff = [&]() -> int {
+	// (mid: enqueued between the member kernel and the chains)
+	auto run_diff = [&](const std::function<int()>& mid) -> int {
 		HIPCHK(ctx, rec(2, st));
 		if (!P->members) HIPCHK(ctx, rec(6, st));
 		EncodeArgs a{};
@@ -1148,6 +1163,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.srec = m.srec;
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 				HIPCHK(ctx, rec(6, st));
+				if (mid) {
+					const int rc = mid();
+					if (rc != DG_OK) return rc;
+				}
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			} else {
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
@@ -1178,22 +1197,37 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	int rc;
 	if (serial) {
 		if ((rc = run_crc()) != DG_OK) return rc;
-		if ((rc = run_diff()) != DG_OK) return rc;
+		if ((rc = run_diff(nullptr)) != DG_OK) return rc;
 	} else if (P->crc_fused || P->crc_wide_beside) {
 		// the build writes R's CRC; V's CRC forks after the build (ev_fork,
 		// recorded by launch_correcting) and runs beside the V scan
-		if ((rc = run_diff()) != DG_OK) return rc;
+		if ((rc = run_diff(nullptr)) != DG_OK) return rc;
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
 		if ((rc = run_crc()) != DG_OK) return rc;
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
+	} else if (P->members && P->crc_join == 1 && !P->crc_first) {
+		// member plans: the CRC runs beside the member kernel and the chains
+		// start after both.  A CRC still dispatching beside the chains
+		// (crc_finalize's waves queued behind a full grid of chains) slowed
+		// the routed chain of c3s by 13 % (40.9 vs 36.2 ms).
+		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
+		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
+		rc = run_diff([&]() -> int {
+			const int r = run_crc();
+			if (r != DG_OK) return r;
+			HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
+			HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
+			return DG_OK;
+		});
+		if (rc != DG_OK) return rc;
 	} else {
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
 		if (P->crc_first) {   // A/B: CRC waves dispatched first
 			if ((rc = run_crc()) != DG_OK) return rc;
-			if ((rc = run_diff()) != DG_OK) return rc;
+			if ((rc = run_diff(nullptr)) != DG_OK) return rc;
 		} else {
-			if ((rc = run_diff()) != DG_OK) return rc;
+			if ((rc = run_diff(nullptr)) != DG_OK) return rc;
 			if ((rc = run_crc()) != DG_OK) return rc;
 		}
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
@@ -1232,6 +1266,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		HIPCHK(ctx, launch_serialize_wave(s, st));
 	}
 	if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs
+	if (late_fin && !P->skip_crc) HIPCHK(ctx, launch_crc_finalize(crc_args(), st));
 	HIPCHK(ctx, launch_crc_patch(d_out, d_offsets, P->d_crc.as<uint64_t>(), d_status, P->n, st));
 	HIPCHK(ctx, rec(5, st));
 	return DG_OK;

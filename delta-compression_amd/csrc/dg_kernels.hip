@@ -377,7 +377,12 @@ hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
 	return hipGetLastError();
 }
 
-hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, int pass) {
+hipError_t launch_crc_finalize(const CrcArgs& a, hipStream_t st) {
+	if (a.n_spans) hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
+	return hipGetLastError();
+}
+
+hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, int pass, bool finalize) {
 	if (a.n_segs) {
 		uint32_t blocks = (a.n_segs + kCrcWavesPerBlock - 1) / kCrcWavesPerBlock;
 		static const uint32_t env_cap = [] {
@@ -391,8 +396,7 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, in
 		else
 			hipLaunchKernelGGL(crc_rows_kernel<kCrcByte>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 	}
-	if (a.n_spans)
-		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
+	if (finalize) return launch_crc_finalize(a, st);
 	return hipGetLastError();
 }
 
@@ -470,7 +474,7 @@ __device__ __forceinline__ bool overlap(uint64_t a, uint64_t al, uint64_t b, uin
 // serial header decodes.  The commands are then applied 64 at a time.
 #ifdef DG_ONEPASS_PROF   // profiling build only (make prof): per-phase decode cycles
 enum { DP_FILL, DP_LOAD, DP_N1, DP_DBL, DP_WALK, DP_EXP, DP_HDR, DP_COPY, DP_WAIT, DP_WINDOWS, DP_BATCHES, DP_TOTAL,
-       DP_ORDERED, DP_C_CMD, DP_C_FLAT, DP_C_BAR, kDecProfN };
+       DP_ORDERED, DP_C_CMD, DP_C_FLAT, DP_C_BAR, DP_CRC_SYNC, DP_CRC_SEG, DP_CRC_TAIL, kDecProfN };
 __device__ unsigned long long g_decode_prof[kDecProfN];
 #define DPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define DPROF_ADD(i, t0) (dprof[(i)] += __builtin_amdgcn_s_memtime() - (t0))
@@ -1010,7 +1014,6 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	}
 	// initial image: R then zeros (in-place, apply.c:276-278) or zeros (apply.c:233)
 	const uint64_t init = inplace ? (rl < bsz ? rl : bsz) : 0;
-	DPROF_T(tf0);
 	// R's CRC-64/XZ from the loads that make the in-place image (R is read
 	// once): 16 KiB segments as rows of 64 x 8 bytes, segment j on wave j % 4,
 	// each wave folding its segments Horner-wise; the image's whole 16-byte
@@ -1019,6 +1022,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	const bool rcrc_early = a.crc_check && aligned_or && rl >= 8;
 	uint64_t racc = 0;
 	uint32_t rlast = ~0u;
+	DPROF_T(tf0);
 	if (rcrc_early) {
 		const DecCrc ct = dec_crc_tables(NX, a);
 		__syncthreads();
@@ -1201,8 +1205,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			c[7] = N1[e6];
 		}
 		__syncthreads();   // cmds complete; N2..N8 dead: NX becomes the copy scratch
-		DPROF_ADD(DP_EXP, te0);
-		// the walk's terminal: x is where it stopped
+		DPROF_ADD(DP_EXP, te0);		// the walk's terminal: x is where it stopped
 		uint64_t next_pos = pos + x;   // kNxCut: restart at x
 		if (term == kNxEnd) done = true;
 		else if (term == kNxBad) st = 8;
@@ -1302,7 +1305,10 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	//    x^(8 * 64 KiB); thread 0 shifts the partials into place. ──
 	int32_t cst = 0;
 	if (a.crc_check && !st) {
+		DPROF_T(tk0);
 		block_sync_global();   // every wave's output stores before any CRC read
+		DPROF_ADD(DP_CRC_SYNC, tk0);
+		DPROF_T(tk1);
 		const uint64_t* Lv = a.tables + 8 * 256;
 		const uint64_t* KF = Lv + kCrcLevels * kCrcNibTabWords;   // x^(8 seg), x^(-8t), x^(8 seg k) k = 2..4
 		// LDS (the dead doubling arrays): the row tables and x^(8 * 64 KiB);
@@ -1333,38 +1339,47 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			}
 		}
 		__syncthreads();
-		if (tid == 0) {
-			uint64_t crc[2];
-			for (int sp = 0; sp < 2; ++sp) {
-				if (sl[sp] < 8) {
-					const uint8_t* d = reinterpret_cast<const uint8_t*>(sa[sp]);
-					uint64_t c = ~0ULL;
-					for (uint64_t k = 0; k < sl[sp]; ++k) c = a.tables[(uint8_t)(c ^ d[k])] ^ (c >> 8);
-					crc[sp] = ~c;
-					continue;
-				}
-				const uint32_t nseg = crc_nseg(sa[sp], sl[sp], kDecCrcSeg);
-				uint64_t raw = 0;
-				for (uint32_t w2 = 0; w2 < kDecWaves; ++w2) {
-					if (clast[sp][w2] == ~0u) continue;
-					const uint32_t k = nseg - 1 - clast[sp][w2];   // 0..3 segments (16, 32, 48 KiB) after its last
-					raw ^= k == 0 ? cpart[sp][w2]
-					              : mul_nib(cpart[sp][w2], k == 1 ? Lv + 4 * kCrcNibTabWords      // x^(8 * 16 KiB)
-					                                       : k == 2 ? Lv + 5 * kCrcNibTabWords    // x^(8 * 32 KiB)
-					                                                : KF + kCrcFinX48K * kCrcNibTabWords);
-				}
-				const uintptr_t end = sa[sp] + sl[sp];
-				const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
-				if (t) raw = mul_nib(raw, KF + (1 + t) * kCrcNibTabWords);   // undo the trailing pad
-				crc[sp] = ~raw;
+		DPROF_ADD(DP_CRC_SEG, tk1);
+		DPROF_T(tk2);
+		// Wave 0 combines, one lane per (span, wave) partial: the shifts
+		// x^(8 * 16 KiB * k) run side by side (one gather round, not eight in
+		// a row on thread 0), then the two spans' pad fixes side by side.
+		if (wave == 0) {
+			const uint32_t sp = lane / kDecWaves, w2 = lane % kDecWaves;
+			uint64_t v = 0;
+			if (lane < 2 * kDecWaves && sl[sp] >= 8 && clast[sp][w2] != ~0u) {
+				const uint32_t k = crc_nseg(sa[sp], sl[sp], kDecCrcSeg) - 1 - clast[sp][w2];   // 0..3 segments after its last
+				v = cpart[sp][w2];
+				if (k)
+					v = mul_nib(v, k == 1 ? Lv + 4 * kCrcNibTabWords      // x^(8 * 16 KiB)
+					               : k == 2 ? Lv + 5 * kCrcNibTabWords    // x^(8 * 32 KiB)
+					                        : KF + kCrcFinX48K * kCrcNibTabWords);
 			}
-			uint64_t sc = 0, dc = 0;
-			for (int k = 0; k < 8; ++k) {
-				sc = (sc << 8) | D[9 + k];
-				dc = (dc << 8) | D[17 + k];
+			const uint64_t raw0 = wave_xor64(lane < kDecWaves ? v : 0ull);
+			const uint64_t raw1 = wave_xor64(lane >= kDecWaves && lane < 2 * kDecWaves ? v : 0ull);
+			bool bad = false;
+			if (lane < 2) {   // lane s: span s (0 = R, 1 = output)
+				const uintptr_t s0 = lane ? sa[1] : sa[0];
+				const uint64_t len = lane ? sl[1] : sl[0];
+				uint64_t c;
+				if (len < 8) {
+					const uint8_t* d = reinterpret_cast<const uint8_t*>(s0);
+					c = ~0ULL;
+					for (uint64_t k = 0; k < len; ++k) c = a.tables[(uint8_t)(c ^ d[k])] ^ (c >> 8);
+				} else {
+					c = lane ? raw1 : raw0;
+					const uintptr_t end = s0 + len;
+					const uint32_t t = (uint32_t)(((end + 15) & ~(uintptr_t)15) - end);
+					if (t) c = mul_nib(c, KF + (1 + t) * kCrcNibTabWords);   // undo the trailing pad
+				}
+				uint64_t h = 0;
+				for (int k = 0; k < 8; ++k) h = (h << 8) | D[9 + 8 * lane + k];
+				bad = h != ~c;
 			}
-			cst = sc != crc[0] ? 9 : (dc != crc[1] ? 10 : 0);
+			const uint64_t bm = __ballot(bad);
+			cst = bm & 1 ? 9 : (bm & 2 ? 10 : 0);
 		}
+		DPROF_ADD(DP_CRC_TAIL, tk2);
 	}
 	if (tid == 0) {
 		a.status[i] = st ? st : cst;

@@ -60,6 +60,26 @@ constexpr uint32_t kLongChunks = 8;
 #endif                    // persistent waves (LDS allows 17)                        // members of up to 512 steps are verified
 static_assert(kStage % 16 == 0, "16-byte blocks");
 
+// Profiling build (DG_LIB_VARIANT=prof, scripts/member_phases.py): per-phase
+// shader-clock cycles and counts of member_chunk_kernel, summed over waves
+#ifdef DG_ONEPASS_PROF
+enum : int { MP_STAGE, MP_MASK, MP_RUNS, MP_SNLAST, MP_SETUP, MP_SHORT, MP_LONG, MP_PREFIX, MP_TOTAL, MP_CHUNKS,
+             MP_MEMBERS, MP_SHORT_N, MP_LONG_N, MP_ROUNDS, MP_UNVER, MP_FLAGGED, MP_D1, kMemProfN };
+constexpr uint32_t kMemProfSlots = 256;   // spread: one set of counters per blockIdx % 256
+__device__ unsigned long long g_member_prof[kMemProfSlots * kMemProfN];
+struct MemProf {
+	uint64_t v[kMemProfN] = {};
+};
+#define MPROF_T(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define MPROF_ADD(k, t) mp.v[k] += __builtin_amdgcn_s_memtime() - (t)
+#define MPROF_INC(k, n) mp.v[k] += (n)
+#else
+struct MemProf {};
+#define MPROF_T(t)
+#define MPROF_ADD(k, t)
+#define MPROF_INC(k, n)
+#endif
+
 // 16 mismatch bits of 16 bytes (bit i: byte i of the chunk differs)
 __device__ __forceinline__ uint32_t mismatch16(const uint4& v, const uint4& r) {
 	const uint32_t x[4] = {v.x ^ r.x, v.y ^ r.y, v.z ^ r.z, v.w ^ r.w};
@@ -130,12 +150,21 @@ struct ChunkLds {
 	uint32_t filt[64];           // V-hash filter of a round or a long member
 };
 
-// the 16 bytes at offset o of a staged stream: one unaligned ds_read_b128
-// (gfx950 runs with unaligned LDS access)
+// the 16 bytes at offset o of a staged stream (s 16-byte aligned): five
+// aligned dwords and four funnel shifts.  gfx950 accepts an unaligned
+// ds_read_b128, but it stalls the LDS pipe: on C3 SQ_LDS_UNALIGNED_STALL was
+// 61 % of the member kernel's LDS-active cycles (profiles/r05_member_census.md).
 __device__ __forceinline__ uint4 lds16(const uint8_t* s, uint32_t o) {
+#ifdef DG_LDS16_UNALIGNED   // A/B variant: the unaligned ds_read_b128
 	uint4 w;
 	__builtin_memcpy(&w, s + o, 16);
 	return w;
+#endif
+	const uint32_t* d = reinterpret_cast<const uint32_t*>(s + (o & ~3u));
+	const uint32_t sh = (o & 3u) * 8u;
+	const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+	return make_uint4(__builtin_amdgcn_alignbit(d1, d0, sh), __builtin_amdgcn_alignbit(d2, d1, sh),
+	                  __builtin_amdgcn_alignbit(d3, d2, sh), __builtin_amdgcn_alignbit(d4, d3, sh));
 }
 
 // An equality-preserving 32-bit hash of a window for check (A): only byte-
@@ -324,18 +353,20 @@ struct JobCursor {
 	uint64_t v_off, r_off, mem_base, q, q_magic, rec_base;
 	template <class Args>
 	__device__ void load_pair(const Args& a) {
+		// (wave-uniform: into SGPRs, so the member kernel's 72-VGPR budget
+		// holds no 64-bit descriptor copies)
 		const PairDev& pd = a.pairs[pair];
 		const PairPlanDev& pp = a.pplan[pair];
-		v_off = pd.v_off;
-		r_off = pd.r_off;
-		vl = (uint32_t)pd.v_len;
-		rl = (uint32_t)pd.r_len;
-		mem_base = pp.mem_base;
-		q = pp.q;
-		q_magic = pp.q_magic;
-		chunk_base = pp.chunk_base;
-		n_chunks = pp.n_chunks;
-		rec_base = pp.rec_base;
+		v_off = uni64(pd.v_off);
+		r_off = uni64(pd.r_off);
+		vl = uni((uint32_t)pd.v_len);
+		rl = uni((uint32_t)pd.r_len);
+		mem_base = uni64(pp.mem_base);
+		q = uni64(pp.q);
+		q_magic = uni64(pp.q_magic);
+		chunk_base = uni(pp.chunk_base);
+		n_chunks = uni(pp.n_chunks);
+		rec_base = uni64(pp.rec_base);
 	}
 	template <class Args>
 	__device__ void start(const Args& a, uint32_t job) {
@@ -406,7 +437,8 @@ __device__ __forceinline__ void stage_store(const SpecArgs& a, const JobCursor& 
 	}
 }
 
-__device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, const JobCursor& J) {
+__device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, const JobCursor& J,
+                                             [[maybe_unused]] MemProf& mp) {
 	const uint32_t lane = lane_id();
 	const uint32_t c = J.c;
 	const uint32_t vl = J.vl, rl = J.rl;
@@ -418,6 +450,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 	// ── 2. mismatch bitmap: bit o = position g0 + o differs (or is E, the
 	//    sentinel); chunk 0's lookbehind holds only the virtual mismatch at -1 ──
 	const int64_t lim = (int64_t)E - g0;   // offset of the sentinel
+	MPROF_T(tm0);
 	for (uint32_t j = lane; j < kMaskWords; j += 64) {
 		const uint32_t o = 32 * j;
 		uint32_t m = 0;
@@ -433,6 +466,8 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 		L.mask[j] = m;
 	}
 	lds_fence();
+	MPROF_ADD(MP_MASK, tm0);
+	MPROF_T(tr0);
 	// ── 3. run starts (offsets >= 16: positions of this chunk and the
 	//    look-ahead) and the running last-mismatch maximum ──
 	uint32_t nrun = g0 < 0 ? 1u : 0u, carry = 0;   // chunk 0: slot 0 is member 0 (position 0)
@@ -471,6 +506,9 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 		nm += (uint32_t)__builtin_popcountll(__ballot(i < nrun && L.run[i] < 16 + kMemChunk));
 	}
 	if (lane == 0) a.n_mem[J.chunk_base + c] = nm;
+	MPROF_ADD(MP_RUNS, tr0);
+	MPROF_INC(MP_MEMBERS, nm);
+	MPROF_T(ts0);
 
 	// The last member when no later run starts in the staged region (sparse
 	// edits: 1 MiB pairs at 1 %): its run has ended once 16 clean bytes follow
@@ -515,6 +553,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 		}
 	}
 
+	MPROF_ADD(MP_SNLAST, ts0);
 	const uint64_t q = J.q, qmag = J.q_magic;
 	const ModQ mq = make_modq(q, qmag);
 	VFilter<64> fs{L.filt};
@@ -524,6 +563,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 	uint32_t vp = 0, vbytes = 0;   // verified prefix of the chunk's members, its delta bytes
 	bool open = true;
 	for (uint32_t k0 = 0; k0 < nm; k0 += 64) {
+		MPROF_T(tb0);
 		// lane m: member k0 + m (offsets; x = last mismatch before the next
 		// run start + 1; a member whose next start is unknown stays unverified)
 		const uint32_t k1 = umin32(k0 + 64, nm);
@@ -556,6 +596,10 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			}
 		}
 
+		MPROF_INC(MP_SHORT_N, __builtin_popcountll(__ballot(shrt)));
+		MPROF_INC(MP_UNVER, __builtin_popcountll(__ballot(mine && (!known || T >= 64u * kLongChunks))));
+		MPROF_ADD(MP_SETUP, tb0);
+		MPROF_T(tq0);
 		// ── short members, packed 64 steps per round (lane = step) ──
 		uint32_t done = 0;
 		for (;;) {
@@ -565,6 +609,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 #ifdef DG_MEM_SKIP_SHORT   // timing variants only
 			break;
 #endif
+			MPROF_INC(MP_ROUNDS, 1);
 			const uint32_t hi = 63u - (uint32_t)__builtin_clzll(RM);
 			const uint32_t B = rdlane(P, hi) - done;   // live steps of the round
 			// lane -> member: a mark at each member's first step, prefix max
@@ -607,6 +652,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 #else
 			for (uint64_t w = __ballot(live && !isT && fs.has(fRl)); w; w &= w - 1) {
 #endif
+				MPROF_INC(MP_FLAGGED, 1);
 				const uint32_t Lx = ffs64(w);
 				const uint64_t others = ((uint64_t)rdlane((uint32_t)(mem >> 32), Lx) << 32 | rdlane((uint32_t)mem, Lx)) &
 				                        ~(1ull << Lx);
@@ -628,6 +674,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 				bool badT = isT && (A1 & mem) != 0;
 				const bool d1 = isT && !badT && (B1 & mem) != 0;
 				if (__ballot(d1)) {   // rare: the R slots
+					MPROF_INC(MP_D1, 1);
 					const uint32_t sR = live ? slot_lds(SR, ms_j + t, mq, q, qmag) : kSentinel - 1u;
 					const uint32_t rT = (uint32_t)__builtin_amdgcn_ds_bpermute(tsel, (int)sR);
 					const uint64_t C1 = __ballot(step && sR == rT);
@@ -653,12 +700,15 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			done += B;
 		}
 
+		MPROF_ADD(MP_SHORT, tq0);
+		MPROF_T(tl0);
 		// ── long members (64 <= T < 512): 64-step rows, history in VGPRs ──
 #ifdef DG_MEM_SKIP_LONG   // timing variants only
 		for (uint64_t LM = 0; LM; LM &= LM - 1) {
 #else
 		for (uint64_t LM = __ballot(known && !shrt && T < 64u * kLongChunks); LM; LM &= LM - 1) {
 #endif
+			MPROF_INC(MP_LONG_N, 1);
 			const uint32_t M = ffs64(LM);
 			const uint32_t s0 = rdlane(s, M), tl = rdlane(T, M), sn0 = rdlane(sn, M);
 			uint32_t pw;
@@ -671,6 +721,8 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			}
 			if (lane == M) myok = ok;
 		}
+		MPROF_ADD(MP_LONG, tl0);
+		MPROF_T(tp0);
 		// the chunk's verified prefix through this batch
 		if (open) {
 			const uint32_t lim2 = k1 - k0;
@@ -682,6 +734,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			vp += take;
 			open = take == lim2;
 		}
+		MPROF_ADD(MP_PREFIX, tp0);
 	}
 	// ── 5. chunk summary for the chain: the verified prefix and its delta
 	//    bytes (accumulated per batch above) ──
@@ -706,6 +759,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_MEM_WAVES
 	const uint32_t lane = lane_id();
 	JobCursor J;
 	J.start(a, a.job0 + blockIdx.x);
+	MemProf mp;
+	MPROF_T(tk0);
 	{
 		const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
 		const uint8_t* V = a.ver + J.v_off;
@@ -728,8 +783,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_MEM_WAVES
 		vm_drain();
 		__syncthreads();
 	}
-	member_chunk(a, L, J);
+	MPROF_ADD(MP_STAGE, tk0);
+	member_chunk(a, L, J, mp);
+#ifdef DG_ONEPASS_PROF
+	MPROF_ADD(MP_TOTAL, tk0);
+	MPROF_INC(MP_CHUNKS, 1);
+	if (lane == 0)
+		for (int k = 0; k < kMemProfN; ++k)
+			atomicAdd(&g_member_prof[(blockIdx.x % kMemProfSlots) * kMemProfN + k], (unsigned long long)mp.v[k]);
+#endif
 }
+
+#ifdef DG_ONEPASS_PROF
+extern "C" int dg_member_prof_read(unsigned long long* out, int n) {
+	if (n > kMemProfN) n = kMemProfN;
+	static unsigned long long h[kMemProfSlots * kMemProfN];
+	if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_member_prof), sizeof h) != hipSuccess) return -1;
+	for (int k = 0; k < n; ++k) {
+		out[k] = 0;
+		for (uint32_t s = 0; s < kMemProfSlots; ++s) out[k] += h[s * kMemProfN + k];
+	}
+	return n;
+}
+extern "C" int dg_member_prof_reset(void) {
+	static unsigned long long z[kMemProfSlots * kMemProfN] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_member_prof), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ── member-mode serialisation ──────────────────────────────────────────
 

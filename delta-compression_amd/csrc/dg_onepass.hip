@@ -1353,6 +1353,13 @@ static bool force_global_src() {
 
 bool onepass16_selected() { return !force_global_src(); }
 
+// DG_OP_LDS_PAD=bytes: dynamic LDS added to the onepass16 launches, which caps
+// the resident chains per CU (A/B builds only: occupancy experiments)
+static uint32_t op_lds_pad() {
+	const char* e = ab_env("DG_OP_LDS_PAD");
+	return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+}
+
 hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
 	if (a.n_pairs == 0) return hipSuccess;
 	if (p == 16 && aligned16 && !force_global_src()) {
@@ -1360,10 +1367,10 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 			// (pairs [pair0, n_pairs): one group of a pipelined run)
 			const uint32_t g = a.n_pairs - a.pair0;
 			if (g == 0) return hipSuccess;
-			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), 0, st, a);
-			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), 0, st, a);
+			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), op_lds_pad(), st, a);
+			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), op_lds_pad(), st, a);
 		} else {
-			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), 0, st, a);
+			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), op_lds_pad(), st, a);
 		}
 	}
 	else if (a.lookback)

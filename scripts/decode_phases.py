@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = ["fill", "win_load", "n1", "doubling", "walk", "expand", "hdr+checks", "copy", "final_wait",
-         "windows", "batches", "total", "ordered_windows", "c_cmd", "c_flat", "c_barrier"]
+         "windows", "batches", "total", "ordered_windows", "c_cmd", "c_flat", "c_barrier", "crc_sync", "crc_seg",
+         "crc_tail"]
 
 
 def main():
