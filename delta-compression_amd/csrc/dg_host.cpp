@@ -5,7 +5,6 @@
 // dg_kernels.hip on one HIP stream, and moves host buffers through pinned
 // staging for the host-memory entry points.  There is no CPU compute
 // fallback: without a GPU every entry point fails with DG_ERR_NO_DEVICE.
-#include <functional>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -422,8 +421,7 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
-	int crc_join = 2;          // member plans: 2 = the CRC's combine after the chains, 1 = the chains
-	                           // wait for the whole CRC, 0 = neither (DG_CRC_JOIN, A/B)
+	bool crc_late_fin = true;  // member plans: the CRC's combine after the chains (DG_CRC_JOIN=0: not, A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
@@ -886,7 +884,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	const char* cf = ab_env("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
 	const char* cj = ab_env("DG_CRC_JOIN");
-	if (cj) P->crc_join = (int)strtol(cj, nullptr, 0);
+	if (cj) P->crc_late_fin = cj[0] != '0';
 	const char* sk = ab_env("DG_SKIP_CRC");
 	P->skip_crc = sk && sk[0] == '1';
 
@@ -1069,7 +1067,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// stream for the chains.  Enqueued right after the row pass, its waves
 	// queue behind the chains' full grid and slowed the routed chain of c3s
 	// by 13 % (40.9 vs 36.2 ms, profiles/r05_experiments.md).
-	const bool late_fin = P->members && P->crc_join == 2 && !serial && !P->crc_wide && !P->fused;
+	const bool late_fin = P->members && P->crc_late_fin && !serial && !P->crc_wide && !P->fused;
 	auto crc_args = [&]() {
 		CrcArgs a{};
 		a.arena[0] = d_ref;
@@ -1109,8 +1107,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		return DG_OK;
 	};
 	// differencing -> COPY records + per-pair delta sizes
-	// (mid: enqueued between the member kernel and the chains)
-	auto run_diff = [&](const std::function<int()>& mid) -> int {
+	auto run_diff = [&]() -> int {
 		HIPCHK(ctx, rec(2, st));
 		if (!P->members) HIPCHK(ctx, rec(6, st));
 		EncodeArgs a{};
@@ -1163,10 +1160,6 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.srec = m.srec;
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 				HIPCHK(ctx, rec(6, st));
-				if (mid) {
-					const int rc = mid();
-					if (rc != DG_OK) return rc;
-				}
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			} else {
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
@@ -1197,37 +1190,22 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	int rc;
 	if (serial) {
 		if ((rc = run_crc()) != DG_OK) return rc;
-		if ((rc = run_diff(nullptr)) != DG_OK) return rc;
+		if ((rc = run_diff()) != DG_OK) return rc;
 	} else if (P->crc_fused || P->crc_wide_beside) {
 		// the build writes R's CRC; V's CRC forks after the build (ev_fork,
 		// recorded by launch_correcting) and runs beside the V scan
-		if ((rc = run_diff(nullptr)) != DG_OK) return rc;
+		if ((rc = run_diff()) != DG_OK) return rc;
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
 		if ((rc = run_crc()) != DG_OK) return rc;
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
-	} else if (P->members && P->crc_join == 1 && !P->crc_first) {
-		// member plans: the CRC runs beside the member kernel and the chains
-		// start after both.  A CRC still dispatching beside the chains
-		// (crc_finalize's waves queued behind a full grid of chains) slowed
-		// the routed chain of c3s by 13 % (40.9 vs 36.2 ms).
-		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
-		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
-		rc = run_diff([&]() -> int {
-			const int r = run_crc();
-			if (r != DG_OK) return r;
-			HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
-			HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));
-			return DG_OK;
-		});
-		if (rc != DG_OK) return rc;
 	} else {
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
 		if (P->crc_first) {   // A/B: CRC waves dispatched first
 			if ((rc = run_crc()) != DG_OK) return rc;
-			if ((rc = run_diff(nullptr)) != DG_OK) return rc;
+			if ((rc = run_diff()) != DG_OK) return rc;
 		} else {
-			if ((rc = run_diff(nullptr)) != DG_OK) return rc;
+			if ((rc = run_diff()) != DG_OK) return rc;
 			if ((rc = run_crc()) != DG_OK) return rc;
 		}
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
