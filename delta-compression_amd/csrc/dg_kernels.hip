@@ -466,11 +466,12 @@ __device__ __forceinline__ bool overlap(uint64_t a, uint64_t al, uint64_t b, uin
 //   1. every lane computes, for each window offset x it owns, the offset of the
 //      next command IF a command started at x (N1), or a code: END, malformed,
 //      header cut by the window, next command past the window;
-//   2. N2 = N1.N1, N4, N8 by pointer doubling (codes propagate);
-//   3. one uniform walk takes 8 commands per step through N8 (single steps
-//      only near the window end), then the nodes in between are expanded in
-//      parallel.
-// So a window of ~300 commands costs ~40 dependent LDS reads instead of ~300
+//   2. N2 = N1.N1, N4, N8, N16 by pointer doubling (codes propagate; N16
+//      takes N4's place once N8 is built);
+//   3. one uniform walk takes 16 commands per step through N16, then at most
+//      one N8 step and single steps near the window end; the nodes in between
+//      are expanded in parallel.
+// So a window of ~300 commands costs ~25 dependent LDS reads instead of ~300
 // serial header decodes.  The commands are then applied 64 at a time.
 #ifdef DG_ONEPASS_PROF   // profiling build only (make prof): per-phase decode cycles
 enum { DP_FILL, DP_LOAD, DP_N1, DP_DBL, DP_WALK, DP_EXP, DP_HDR, DP_COPY, DP_WAIT, DP_WINDOWS, DP_BATCHES, DP_TOTAL,
@@ -948,7 +949,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	// N2, N4, N8 during the parse; the waves' flat-copy scratch afterwards
 	__shared__ __attribute__((aligned(16))) uint16_t NX[3 * kDecWin];
 	__shared__ uint16_t cmds[kDecMaxCmds];
-	__shared__ uint16_t jumps[kDecMaxCmds / 8 + 1];
+	__shared__ uint16_t jumps[kDecMaxCmds / 16 + 2];   // 16-command jumps, then the one 8-command jump
 	__shared__ uint32_t sh[8];   // walk results and window flags
 	__shared__ uint32_t bsum[2 * (kDecMaxCmds / 64 + 1)];   // per batch: first written dst, max end
 	__shared__ uint64_t cpart[2][kDecWaves];   // crc_check: per span, each wave's Horner partial
@@ -956,6 +957,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 	uint16_t* N2 = NX;
 	uint16_t* N4 = NX + kDecWin;
 	uint16_t* N8 = NX + 2 * kDecWin;
+	uint16_t* N16 = N4;   // (N4 is dead once N8 is built)
 	constexpr uint32_t kScratch = 64 * 4 + 128 * 4 + 64 * 8 + 64 * 8 + 64 * 4;
 	static_assert(kDecWaves * kScratch <= 3 * kDecWin * 2, "scratch fits NX");
 	DecScratch xs;
@@ -1153,20 +1155,32 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 		__syncthreads();
 		dbl(N4, N8);
 		__syncthreads();
+		dbl(N8, N16);
+		__syncthreads();
 		DPROF_ADD(DP_DBL, td0);
 		DPROF_T(tw0);
-		// ── 4. the walk (wave 0, uniform): 8 commands per N8 step, then single steps ──
+		// ── 4. the walk (wave 0, uniform): 16 commands per N16 step, at most
+		//    one N8 step, then single steps ──
 		if (wave == 0) {
-			uint32_t x = 0, nj = 0;
+			uint32_t x = 0, nj = 0, n8 = 0;
 			uint32_t term = 0;
 			while (true) {
-				const uint32_t y = uni(N8[x]);
-				if (y >= kNxSpecial || 8 * (nj + 1) > kDecMaxCmds) break;
+				const uint32_t y = uni(N16[x]);
+				if (y >= kNxSpecial || 16 * (nj + 1) > kDecMaxCmds) break;
 				if (lane == 0) jumps[nj] = (uint16_t)x;
 				++nj;
 				x = y;
 			}
-			uint32_t cnt = 8 * nj;
+			uint32_t cnt = 16 * nj;
+			{
+				const uint32_t y = uni(N8[x]);
+				if (y < kNxSpecial && cnt + 8 <= kDecMaxCmds) {
+					if (lane == 0) jumps[nj] = (uint16_t)x;
+					n8 = 1;
+					cnt += 8;
+					x = y;
+				}
+			}
 			while (true) {   // single steps from x (at most 7 commands + the terminal)
 				const uint32_t y = uni(N1[x]);
 				if (y == kNxEnd || y == kNxBad || y == kNxCut) { term = y; break; }
@@ -1183,18 +1197,22 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 				sh[3] = term;
 				sh[4] = 0;   // a batch out of bounds
 				sh[5] = 0;   // the window is not order-free
+				sh[6] = n8;
 			}
 		}
 		__syncthreads();
-		const uint32_t cnt = sh[0], nj = sh[1], x = sh[2], term = sh[3];
+		const uint32_t cnt = sh[0], nj = sh[1], x = sh[2], term = sh[3], n8 = sh[6];
 		DPROF_ADD(DP_WALK, tw0);
 		DPROF_T(te0);
-		// expand the jumps: the 8 nodes from jumps[j]
-		for (uint32_t j = tid; j < nj; j += kDecBlock) {
-			const uint32_t e0 = jumps[j];
-			const uint32_t e2 = N2[e0], e4 = N4[e0];
+		// expand the jumps: 8 nodes from each base (e, N1 e, N2 e, ..., N1 N2 N2 N2 e);
+		// a 16-command jump has bases e and N8 e
+		for (uint32_t k = tid; k < 2 * nj + n8; k += kDecBlock) {
+			const uint32_t j = k >> 1;
+			const uint32_t e0 = j < nj ? ((k & 1) ? N8[jumps[j]] : jumps[j]) : jumps[nj];
+			const uint32_t e2 = N2[e0];
+			const uint32_t e4 = N2[e2];
 			const uint32_t e6 = N2[e4];
-			uint16_t* c = cmds + 8 * j;
+			uint16_t* c = cmds + (j < nj ? 16 * j + 8 * (k & 1) : 16 * nj);
 			c[0] = (uint16_t)e0;
 			c[1] = N1[e0];
 			c[2] = (uint16_t)e2;
