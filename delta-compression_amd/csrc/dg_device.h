@@ -216,6 +216,7 @@ struct SerArgs {
 	uint64_t out_cap;
 	int32_t* status;
 	uint32_t n_pairs;
+	uint32_t crc_in;           // the CRCs are final: write header bytes 9..24 here (no crc_patch_kernel)
 };
 
 struct CrcArgs {

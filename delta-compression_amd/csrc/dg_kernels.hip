@@ -305,8 +305,6 @@ hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* s
 	return hipGetLastError();
 }
 
-// header bytes 9..24 (src/dst CRC, big-endian, encoding.c:52-54) of deltas
-// serialised before their CRCs were known
 // One wave per pair (dg_serialize_wave.h): DPP scans instead of block
 // barriers, 64 commands per tile staged in a 4 KiB LDS slice, so 32 pairs
 // per CU are in flight and their record / payload loads overlap.  The header
@@ -331,8 +329,17 @@ __global__ __launch_bounds__(64) void serialize_wave_kernel(SerArgs s) {
 	                                                 (uint32_t)pd.v_len, s.rec + (uint64_t)s.rec_words * pp.rec_base,
 	                                                 s.rec_words, s.n_rec[pair], (sw_lds8*)stage);
 	if (st != 0 && lane_id() == 0) s.status[pair] = st;
+	if (st == 0 && s.crc_in) {   // header bytes 9..24: CRC of R, CRC of V, big-endian (encoding.c:52-54)
+		const uint32_t lane = lane_id();
+		if (lane < 16) {
+			const uint64_t c = s.crc[2ull * pair + (lane >> 3)];
+			s.out[base + 9 + lane] = (uint8_t)(c >> (56 - 8 * (lane & 7)));
+		}
+	}
 }
 
+// header bytes 9..24 (src/dst CRC, big-endian, encoding.c:52-54) of deltas
+// serialised before their CRCs were known
 __global__ __launch_bounds__(256) void crc_patch_kernel(uint8_t* out, const uint64_t* offsets,
                                                         const uint64_t* crc, const int32_t* status,
                                                         uint32_t n) {
