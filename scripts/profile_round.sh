@@ -18,7 +18,7 @@ export TMPDIR=/tmp
 if [ "$WHAT" = ks ] || [ "$WHAT" = all ]; then
   for c in $CFGS; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ks_$c -o run -- \
-        python3 bench.py --config $c --also none --steps 20 --warmup 5 --no-cpu-baseline \
+        python3 bench.py --config $c --also none --steps 20 --warmup 5 --no-cpu-baseline --no-e2e \
         --full-out $O/ks_$c/bench_full.json > $O/ks_$c.log 2>&1 || { echo "ks $c rc=$?"; tail -5 $O/ks_$c.log; exit 1; }
     tail -1 $O/ks_$c.log | cut -c1-200
   done
@@ -44,7 +44,7 @@ if [ "$WHAT" = pmc ] || [ "$WHAT" = all ]; then
     esac
     for p in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "$K" --output-format csv -d $O/pmc_${c}_$p -o pmc -- \
-          python3 bench.py --config $c --also none --steps 5 --warmup 1 --no-cpu-baseline \
+          python3 bench.py --config $c --also none --steps 5 --warmup 1 --no-cpu-baseline --no-e2e \
           --full-out $O/pmc_${c}_$p.json > $O/pmc_${c}_$p.log 2>&1 || { echo "pmc $c $p rc=$?"; tail -5 $O/pmc_${c}_$p.log; exit 1; }
     done
     echo "pmc $c done"
