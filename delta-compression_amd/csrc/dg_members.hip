@@ -516,7 +516,10 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 	// first mismatch past the region (or the end E, the sentinel), found here
 	// from HBM, and that position is the next run start (>= 16 clean bytes
 	// before it) in a later chunk.  Without it the member stays unverified and
-	// the chain runs the exact epoch machinery from it.
+	// the chain runs the exact epoch machinery from it.  The search is capped
+	// at kSnScanRows KiB past the region (one dependent round trip per KiB):
+	// past the cap the member stays unverified, as before.
+	constexpr uint32_t kSnScanRows = 16;
 	uint32_t sn_last = 0;   // its next run start (offset from g0), 0: unknown
 	if (nm > 0 && nm == nrun && (int64_t)E > g0 + (int64_t)kStage) {
 		const uint32_t xl = L.last[kMaskWords - 1];   // last mismatch + 1 (the sentinel is past the region)
@@ -524,7 +527,8 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			const uint8_t* V = a.ver + J.v_off;
 			const uint8_t* R = a.ref + J.r_off;
 			uint32_t y = ~0u;
-			for (uint64_t b = (uint64_t)(g0 + (int64_t)kStage); y == ~0u; b += 1024) {
+			const uint64_t b_end = (uint64_t)(g0 + (int64_t)kStage) + 1024ull * kSnScanRows;
+			for (uint64_t b = (uint64_t)(g0 + (int64_t)kStage); y == ~0u && b < b_end; b += 1024) {
 				if (b >= E) { y = E; break; }
 				const uint64_t p0 = b + 16ull * lane;
 				uint32_t m = 0;   // bit k: byte p0 + k differs (or is at/after E)
@@ -549,7 +553,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 					y = yy < E ? (uint32_t)yy : E;
 				}
 			}
-			sn_last = (uint32_t)((int64_t)y - g0);
+			if (y != ~0u) sn_last = (uint32_t)((int64_t)y - g0);
 		}
 	}
 

@@ -67,10 +67,12 @@ def _sparse_pairs(seed):
     (dg_members.hip: chunk c stages positions [2048 c - 16, 2048 c + 2288)):
     the chunk's last run then has no later run start staged, and its COPY
     runs to a mismatch found past the region -- just past it, several chunks
-    later, at a stream end, or to an identical tail."""
+    later, at a stream end, or to an identical tail.  The search stops 16 KiB
+    past the region (the member then stays unverified): k = 16383 / 16384 /
+    16400 sit at that cap."""
     rng = random.Random(seed)
     out = []
-    for k in (0, 1, 2, 15, 16, 17, 100, 700, 3000, 9000):
+    for k in (0, 1, 2, 15, 16, 17, 100, 700, 3000, 9000, 16383, 16384, 16400):
         L = 65536 + rng.randrange(2) * rng.randrange(1, 4096)
         R = rng.randbytes(L)
         V = bytearray(R)
@@ -108,9 +110,8 @@ def test_members_sparse_chunk_ends(dg, ctx_mode, orc, q):
 
 
 def _sparse_runs(seed):
-    """Pairs whose deltas are a few percent of V: the member serialiser then
-    reads ADD payloads straight from V (dg_members.hip, direct mode) instead of
-    staging each chunk.  Edits are runs of 1..300 bytes, so the payloads take
+    """Pairs whose deltas are a few percent of V (a sparse batch for the
+    member serialiser).  Edits are runs of 1..300 bytes, so the payloads take
     every copy path (the 4-byte head, 4-byte words, 16-byte pieces, the
     wave-wide copy), some ending right before a chunk or stream boundary."""
     rng = random.Random(seed)
@@ -135,7 +136,7 @@ def test_members_sparse_payload_runs(dg, ctx_mode, orc, q):
     pairs = _sparse_runs(11 + q)
     got = dg.encode_batch([(R, V) for _, R, V in pairs], "onepass", p=16, q=q, ctx=ctx_mode)
     total = sum(len(d) for d in got)
-    assert total * 8 < sum(len(V) for _, _, V in pairs)   # a sparse batch: the direct serialiser
+    assert total * 8 < sum(len(V) for _, _, V in pairs)   # a sparse batch
     for (name, R, V), d in zip(pairs, got):
         assert d == orc.encode(ONEPASS, R, V, p=16, q=q), name
         assert dg.decode(R, d, ctx=ctx_mode) == V, name
