@@ -173,6 +173,19 @@ struct RecWords {   // the record arrays: W words per record, ADD head in the 4t
 // from `out`; prev_end = the V position the first gap starts at.  kCmd
 // records per lane per tile (64 * kCmd commands per tile: fewer dependent
 // load rounds).  Returns the bytes written.
+// The next tile's record words are loaded behind the compiler's back and
+// waited for by hand with vmcnt(kTileStores): loads and stores share the one
+// vmcnt counter, which drains in issue order, so the compiler's own wait at
+// the records' use (placed after this tile's stores, uncountable across the
+// loop) waited for every store to land; serialize_wave_kernel 40.1 -> 35.7 us
+// at C2 (profiles/r05_experiments.md).  The wait holds the registers ("+v"),
+// so nothing reads them before it.
+__device__ __forceinline__ uint32_t rec_load(const uint32_t* p) {
+	uint32_t v;
+	asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+	return v;
+}
+
 template <uint32_t kStageBytes, int kCmd, class Src>
 __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_t vl, const Src& src, uint32_t n,
                                          uint32_t prev_end, sw_lds8* stage) {
@@ -182,6 +195,23 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 	// the next tile's records are loaded while this tile is assembled: their
 	// latency hides under this tile's payload loads
 	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd], ncw[kCmd];
+	static_assert(kCmd == 1 && kStageBytes == 4096, "the hand-counted wait below: 18 stores per tile");
+	constexpr uint32_t kTileStores = kStageBytes / 256 + 2;   // head bytes, dwords, tail bytes
+	static_assert(kTileStores == 18, "vmcnt(18)");
+	constexpr bool kAsm = !Src::kAlwaysHead;
+	auto load_tile = [&](uint32_t t) {   // records t + lane (clamped: every lane loads)
+		const uint32_t j = umin32(t + lane, n - 1);
+		const uint32_t* r = src.rec + (uint64_t)src.W * j;
+		ncv[0] = rec_load(r);
+		ncr[0] = rec_load(r + 1);
+		ncl[0] = rec_load(r + 2);
+		ncw[0] = src.W >= 4 ? rec_load(r + 3) : 0u;
+	};
+	if constexpr (kAsm) {
+		ncv[0] = ncr[0] = ncl[0] = ncw[0] = 0;
+		if (n) load_tile(0);
+		asm volatile("s_waitcnt vmcnt(0)" : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])::"memory");
+	} else
 #pragma unroll
 	for (int i = 0; i < kCmd; ++i) {
 		const uint32_t j = kCmd * lane + i;
@@ -200,8 +230,12 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 			cl[i] = ncl[i];
 			cw[i] = ncw[i];
 			const uint32_t jn = j + 64 * kCmd;
+			if constexpr (kAsm) continue;
 			ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
 			if (jn < n) src.load(jn, ncv[i], ncr[i], ncl[i], ncw[i]);
+		}
+		if constexpr (kAsm) {
+			if (t0 + 64 < n) load_tile(t0 + 64);
 		}
 		// the lane's last valid command end, and the lane's byte count
 		uint32_t last = 0, sz = 0;
@@ -227,28 +261,47 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 			put_cmds<kCmd>(stage, valid, my, prev, cv, cr, cl, cw, inl, V, vl);
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // staged bytes are in LDS
 			__builtin_amdgcn_wave_barrier();
-			// flush: head bytes to a dword boundary, dwords, tail bytes
+			// flush: head bytes to a dword boundary, dwords, tail bytes, as
+			// buffer stores of a fixed count per tile (kTileStores): lanes past
+			// the end are dropped by the descriptor's size, so no store sits in
+			// a branch and the next tile's record wait can count them
 			uint8_t* dst = out + pos;
 			const uint32_t head = (uint32_t)((4u - ((uintptr_t)dst & 3u)) & 3u);
-			if (lane < head && lane < S) dst[lane] = stage[lane];
-			if (S > head) {
-				const uint32_t nd = (S - head) / 4;
-				uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
-				for (uint32_t k = lane; k < nd; k += 64) {
+			{
+				typedef __attribute__((address_space(3))) const uint32_t sw_lds32c;
+				const uint32_t hb = umin32(head, S);
+				const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)hb, 0x00020000);
+				__builtin_amdgcn_raw_buffer_store_b8(stage[lane & 3u], rh, (int)lane, 0, 0);
+				const uint32_t nd = S > head ? (S - head) / 4 : 0u;
+				const __amdgpu_buffer_rsrc_t rd =
+				    __builtin_amdgcn_make_buffer_rsrc(dst + head, (short)0, (int)(4 * nd), 0x00020000);
+#pragma unroll
+				for (uint32_t i = 0; i < kStageBytes / 256; ++i) {
+					const uint32_t k = lane + 64 * i;
 					const uint32_t o = head + 4 * k;
-					typedef __attribute__((address_space(3))) const uint32_t sw_lds32c;
-					const sw_lds32c* w = (const sw_lds32c*)(stage + (o & ~3u));
-					dw[k] = __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
+					const uint32_t oc = o < kStageBytes ? o : 0u;
+					const sw_lds32c* w = (const sw_lds32c*)(stage + (oc & ~3u));
+					__builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(w[1], w[0], oc & 3u), rd, (int)(4 * k), 0, 0);
 				}
-				const uint32_t tail0 = head + 4 * nd;
-				if (lane < S - tail0) dst[tail0 + lane] = stage[tail0 + lane];
+				const uint32_t tail0 = umin32(head + 4 * nd, S);
+				const __amdgpu_buffer_rsrc_t rt =
+				    __builtin_amdgcn_make_buffer_rsrc(dst + tail0, (short)0, (int)(S - tail0), 0x00020000);
+				__builtin_amdgcn_raw_buffer_store_b8(stage[umin32(tail0 + (lane & 3u), kStageBytes)], rt, (int)lane, 0, 0);
 			}
 			__builtin_amdgcn_s_waitcnt(0xc07f);   // LDS reads done before the next tile
 			__builtin_amdgcn_wave_barrier();
 		} else {
 			put_cmds<kCmd>(out + pos, valid, my, prev, cv, cr, cl, cw, inl, V, vl);
+			// (rare: a tile over the stage) its stores drained here, so at
+			// most kTileStores stores are pending at the next tile's wait
+			__builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
 		}
 		pos += S;
+		// the next tile's records: issued before this tile's 18 buffer stores
+		// (a tile past the stage drained its stores with vmcnt(0)), so
+		// vmcnt(18) covers them and no store
+		if constexpr (kAsm)
+			asm volatile("s_waitcnt vmcnt(18)" : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])::"memory");
 		{   // lanes past the end hold last = 0: take the highest lane with a command
 			const uint64_t has = __ballot(valid[0]);
 			if (has) prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
