@@ -195,9 +195,9 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 	// the next tile's records are loaded while this tile is assembled: their
 	// latency hides under this tile's payload loads
 	uint32_t ncv[kCmd], ncr[kCmd], ncl[kCmd], ncw[kCmd];
-	static_assert(kCmd == 1 && kStageBytes == 4096, "the hand-counted wait below: 18 stores per tile");
+	static_assert(kCmd == 1, "one record per lane per tile (the hand-counted wait below)");
 	constexpr uint32_t kTileStores = kStageBytes / 256 + 2;   // head bytes, dwords, tail bytes
-	static_assert(kTileStores == 18, "vmcnt(18)");
+	static_assert(kTileStores <= 63, "vmcnt holds 6 bits");
 	constexpr bool kAsm = !Src::kAlwaysHead;
 	auto load_tile = [&](uint32_t t) {   // records t + lane (clamped: every lane loads)
 		const uint32_t j = umin32(t + lane, n - 1);
@@ -297,11 +297,14 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 			__builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
 		}
 		pos += S;
-		// the next tile's records: issued before this tile's 18 buffer stores
-		// (a tile past the stage drained its stores with vmcnt(0)), so
-		// vmcnt(18) covers them and no store
+		// the next tile's records: issued before this tile's kTileStores
+		// buffer stores (a tile past the stage drained its stores with
+		// vmcnt(0)), so vmcnt(kTileStores) covers them and no store
 		if constexpr (kAsm)
-			asm volatile("s_waitcnt vmcnt(18)" : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])::"memory");
+			asm volatile("s_waitcnt vmcnt(%4)"
+			             : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])
+			             : "n"(kTileStores)
+			             : "memory");
 		{   // lanes past the end hold last = 0: take the highest lane with a command
 			const uint64_t has = __ballot(valid[0]);
 			if (has) prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
