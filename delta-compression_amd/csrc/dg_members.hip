@@ -688,7 +688,11 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			}
 			// verdict at each member's T step; the record carries the ADD head
 			// (the first step's V window) and the COPY length
+			// verdicts and records on the member lanes themselves (no gathers):
+			// member m's steps are lanes [P - T - 1 - done, P - done) of the
+			// round; its ADD head is the first word of its first V window
 			const uint64_t BA = __ballot(bad);
+#ifdef DG_MEM_GATHER_VERDICT   // A/B: the round-4 form (three ds_bpermute per round)
 			const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fb << 2), (int)w0);
 			const uint32_t snj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)sn);   // its next start
 			if (isT) {
@@ -701,6 +705,16 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 				const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((P - done - 1u) << 2), (int)vT);
 				if (in) myok = got != 0u;
 			}
+#else
+			if (in) {
+				const bool ok = (BA & lanes_mask(P - T - 1u - done, T + 1u)) == 0;
+				const uint32_t* d = reinterpret_cast<const uint32_t*>(SV + (s & ~3u));
+				const uint32_t head = __builtin_amdgcn_alignbit(d[1], d[0], (s & 3u) * 8u);
+				*(uint4*)(srec + 4 * lane) = make_uint4((uint32_t)(g0 + (int64_t)(s + T)), sn - (s + T), head, ok ? 1u : 0u);
+				myok = ok;
+			}
+			(void)w0;
+#endif
 			done += B;
 		}
 
