@@ -632,7 +632,7 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			const uint32_t ms_j = inf & 0xFFFu, mt_j = (inf >> 12) & 63u, fb = inf >> 18;
 			const uint32_t t = lane - fb;
 			const bool isT = live && t == mt_j;
-			uint32_t sV = kSentinel, fVl = 0, fRl = 1, w0 = 0;   // (fVl, fRl: window hashes)
+			uint32_t sV = kSentinel, fVl = 0, fRl = 1;   // (fVl, fRl: window hashes)
 			if (live) {
 				const uint4 wv = lds16(SV, ms_j + t), wr = lds16(SR, ms_j + t);
 #ifdef DG_MEM_SKIP_FP   // timing variants only: no fingerprints
@@ -642,7 +642,6 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 #endif
 				fVl = win_hash(wv);
 				fRl = win_hash(wr);
-				w0 = wv.x;
 			}
 #ifndef DG_MEM_SKIP_A
 			if (live && !isT) fs.add(fVl);
@@ -692,20 +691,6 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 			// member m's steps are lanes [P - T - 1 - done, P - done) of the
 			// round; its ADD head is the first word of its first V window
 			const uint64_t BA = __ballot(bad);
-#ifdef DG_MEM_GATHER_VERDICT   // A/B: the round-4 form (three ds_bpermute per round)
-			const uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fb << 2), (int)w0);
-			const uint32_t snj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mj << 2), (int)sn);   // its next start
-			if (isT) {
-				const uint32_t xx = (uint32_t)(g0 + (int64_t)(ms_j + mt_j));
-				const uint32_t v = (BA & mem) == 0 ? 1u : 0u;
-				*(uint4*)(srec + 4 * mj) = make_uint4(xx, snj - (ms_j + mt_j), pw, v);
-			}
-			{   // each member lane takes its verdict from its T step's lane
-				const uint32_t vT = isT && (BA & mem) == 0 ? 1u : 0u;
-				const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((P - done - 1u) << 2), (int)vT);
-				if (in) myok = got != 0u;
-			}
-#else
 			if (in) {
 				const bool ok = (BA & lanes_mask(P - T - 1u - done, T + 1u)) == 0;
 				const uint32_t* d = reinterpret_cast<const uint32_t*>(SV + (s & ~3u));
@@ -713,8 +698,6 @@ __device__ __forceinline__ void member_chunk(const SpecArgs& a, ChunkLds& L, con
 				*(uint4*)(srec + 4 * lane) = make_uint4((uint32_t)(g0 + (int64_t)(s + T)), sn - (s + T), head, ok ? 1u : 0u);
 				myok = ok;
 			}
-			(void)w0;
-#endif
 			done += B;
 		}
 
