@@ -567,8 +567,22 @@ __device__ __forceinline__ uint32_t hdr_be32(const uint32_t (&h)[4], int i) {
 	return __builtin_bswap32(__builtin_amdgcn_alignbyte(h[i + 1], h[i], 1));
 }
 
+// 16 window bytes at any offset as five aligned dwords and four funnel
+// shifts (an unaligned ds_read_b128 stalls the LDS pipe on gfx950,
+// profiles/r05_member_census.md; here decode_kernel 0.1115 -> 0.1088 ms at
+// C5); the window has 32 bytes of slack.
+__device__ __forceinline__ void win16(const uint8_t* p, uint32_t (&h)[4]) {
+	const uint32_t mis = (uint32_t)(uintptr_t)p & 3u;
+	const uint32_t* d = reinterpret_cast<const uint32_t*>(p - mis);
+	const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4], sh = 8u * mis;
+	h[0] = __builtin_amdgcn_alignbit(d1, d0, sh);
+	h[1] = __builtin_amdgcn_alignbit(d2, d1, sh);
+	h[2] = __builtin_amdgcn_alignbit(d3, d2, sh);
+	h[3] = __builtin_amdgcn_alignbit(d4, d3, sh);
+}
+
 // The window holds >= 16 bytes past any command offset (win has 32 bytes of
-// slack), so a header is one unaligned 16-byte LDS read.
+// slack), so a header is one 16-byte read.
 template <typename WP>
 __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b, uint32_t cnt, uint64_t pos) {
 	DecCmd c{false, 0, 0, 0, 0};
@@ -577,7 +591,7 @@ __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b
 	if (c.mine) {
 		const uint32_t cx = cmds[b + lane];
 		uint32_t h[4];
-		__builtin_memcpy(h, w + cx, 16);
+		win16(w + cx, h);
 		c.kind = h[0] & 0xFFu;
 		if (c.kind == 1) {
 			c.src = hdr_be32(h, 0);
@@ -767,7 +781,7 @@ __device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uin
 		if (c < cnt) {
 			const uint32_t cx = cmds[c];
 			uint32_t h[4];
-			__builtin_memcpy(h, w + cx, 16);
+			win16(w + cx, h);
 			const bool copy = (h[0] & 0xFFu) == 1u;
 			const uint32_t src = copy ? hdr_be32(h, 0) : cx + 9u;
 			const uint32_t dst = copy ? hdr_be32(h, 1) : hdr_be32(h, 0);
@@ -1107,7 +1121,7 @@ __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8)
 			dst[0] = make_uint4(bb, bb, bb, bb);
 			dst[1] = make_uint4(bb, bb, bb, bb);
 			uint32_t d[4];
-			__builtin_memcpy(d, w + x0, 16);
+			win16(w + x0, d);
 			uint32_t cand = 0;
 #pragma unroll
 			for (uint32_t k = 0; k < 16; ++k) cand |= (((d[k >> 2] >> (8 * (k & 3))) & 0xFFu) <= 2u ? 1u : 0u) << k;
