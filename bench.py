@@ -104,6 +104,16 @@ CPU_SAMPLE = {"c2": (1024, 4096), "c3": (64, 512), "c4": (64, 512), "c5": (1024,
               "c3s": (32, 256), "c4o": (64, 512), "c6": (64, 256), "c2_defq": (1024, 4096)}
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+# In the timed steps the kernel events are recorded on every TIMING_EVERY-th
+# step only: each event costs its stream ~3.5 us (C2's two per step cost the
+# line ~1.5 %); the average launch time comes from those sampled launches.
+TIMING_EVERY = 4
+
+
+def timing_ring(steps, every=TIMING_EVERY):
+    """(every, slots): the ring holds exactly the sampled timed steps."""
+    every = max(1, min(every, steps))
+    return every, max(1, steps // every)
 
 
 def load_product():
@@ -384,8 +394,11 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     # recorded; the full stage breakdown comes from an untimed pass of the
     # same steps afterwards.  (The ring keeps the last K runs: the timed ones.)
     timing = getattr(args, "stage_timing", "dominant")
+    every, slots = timing_ring(args.steps, getattr(args, "timing_every", TIMING_EVERY))
     if timing != "none":
-        plan.set_timing(args.steps, dominant_only=timing == "dominant")
+        plan.set_timing(slots, dominant_only=timing == "dominant", every=every)
+    else:
+        plan.set_timing(0)
     for _ in range(args.warmup):
         step()
     elapsed = timed(R, args, step)
@@ -468,6 +481,7 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "algorithmic_bytes_per_launch": in_bytes_rank,
             "algorithmic_bytes_per_pair": "|R| + |V| (both streams read once)",
             "avg_launch_ms": round(diff_ms, 4),
+            "timed_launches_sampled": f"events on every {every}th timed step ({slots} launches)",
             "timing": ("HIP events on the run stream after the member kernel and after the chain "
                        "kernels (member chain, routed plain chain), mean over the timed steps"
                        if chains_dominate else
@@ -570,7 +584,8 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
     if int(status.abs().sum()) != 0 or not torch.equal(out[:ver.numel()], ver):
         raise SystemExit(f"{name}: decode failed: status {status.unique().tolist()}")
     yield None   # prepared
-    plan.set_timing(args.steps)
+    every, slots = timing_ring(args.steps, getattr(args, "timing_every", TIMING_EVERY))
+    plan.set_timing(slots, every=every)
     for _ in range(args.warmup):
         step()
     elapsed = timed(R, args, step)
@@ -617,6 +632,7 @@ def bench_decode(name, args, R, dg, ctx, shard, stream):
                      "design_bytes_per_stream": "|delta| + |R| + 3 |V| (R image with R's CRC, COPY "
                                                 "sources, output, the output CRC re-read)",
                      "avg_launch_ms": round(dec_ms, 4),
+                     "timed_launches_sampled": f"events on every {every}th timed step ({slots} launches)",
                      "stage_ms": {k: round(v, 4) for k, v in stages.items()},
                      "path_bytes_per_step": alg,
                      "path_achieved": round(alg / step_s / 1e9, 2),

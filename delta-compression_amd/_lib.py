@@ -138,6 +138,7 @@ def _load() -> C.CDLL:
         "dg_encode_plan_run": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_encode_plan_set_timing": (C.c_int, [vp, C.c_int]),
         "dg_encode_plan_set_timing_mode": (C.c_int, [vp, C.c_int]),
+        "dg_encode_plan_set_timing_every": (C.c_int, [vp, C.c_int]),
         "dg_encode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
         "dg_encode_plan_copy_counts_device": (vp, [vp]),
         "dg_encode_plan_destroy": (None, [vp]),
@@ -158,6 +159,7 @@ def _load() -> C.CDLL:
         "dg_decode_plan_create": (C.c_int, [vp, C.POINTER(DecodeDesc), u32, C.c_int, C.POINTER(vp)]),
         "dg_decode_plan_run": (C.c_int, [vp, vp, vp, vp, vp, vp, vp]),
         "dg_decode_plan_set_timing": (C.c_int, [vp, C.c_int]),
+        "dg_decode_plan_set_timing_every": (C.c_int, [vp, C.c_int]),
         "dg_decode_plan_stage_times": (C.c_int, [vp, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
         "dg_decode_plan_destroy": (None, [vp]),
         "dg_delta_info": (C.c_int, [u8p, sz, C.POINTER(DeltaInfo)]),
@@ -186,6 +188,13 @@ def _load() -> C.CDLL:
 
 
 lib = _load()
+
+
+def _set_every(fn, plan, every):
+    if fn is not None:
+        plan.ctx.check(fn(plan.handle, int(every)), "timing stride")
+    elif every != 1:   # (older A/B variant builds lack it)
+        raise RuntimeError("this library build records events on every run only")
 
 
 def status_string(code: int) -> str:
@@ -289,12 +298,14 @@ class EncodePlan:
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)
 
-    def set_timing(self, slots: int = 1, dominant_only: bool = False):
+    def set_timing(self, slots: int = 1, dominant_only: bool = False, every: int = 1):
         """Record per-stage events for the next runs (ring of `slots` sets);
-        dominant_only: only the events around the dominant kernel(s)."""
+        dominant_only: only the events around the dominant kernel(s);
+        every: only every `every`-th run records them."""
         mode = getattr(lib, "dg_encode_plan_set_timing_mode", None)   # (older A/B variant builds lack it)
         if mode is not None:
             self.ctx.check(mode(self.handle, 1 if dominant_only else 0), "timing mode")
+        _set_every(getattr(lib, "dg_encode_plan_set_timing_every", None), self, every)
         self.ctx.check(lib.dg_encode_plan_set_timing(self.handle, int(slots)), "set_timing")
 
     def stage_times(self):
@@ -342,7 +353,9 @@ class DecodePlan:
         self.ctx.check(lib.dg_decode_plan_run(self.handle, d_ref, d_delta, d_out, d_out_len, d_status,
                                               stream or None), "dg_decode_plan_run")
 
-    def set_timing(self, slots: int = 1):
+    def set_timing(self, slots: int = 1, every: int = 1):
+        """Events around the kernel on every `every`-th run (ring of `slots`)."""
+        _set_every(getattr(lib, "dg_decode_plan_set_timing_every", None), self, every)
         self.ctx.check(lib.dg_decode_plan_set_timing(self.handle, int(slots)), "set_timing")
 
     def stage_times(self):

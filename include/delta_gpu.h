@@ -202,11 +202,15 @@ int dg_encode_plan_run(dg_encode_plan_t *plan,
  * ("members"), the correcting build and scan ("corr_build", "corr_scan",
  * "diff") or the onepass kernel ("diff") — and stage_times reports those
  * only: each timing event costs the run stream a few microseconds, so a
- * throughput measurement records as few as it needs. */
+ * throughput measurement records as few as it needs.
+ * dg_encode_plan_set_timing_every(plan, k), k >= 1: only every k-th run
+ * (the first after set_timing, then every k-th) records its events; the
+ * ring then holds the last `slots` recorded runs.  Resets the run count. */
 #define DG_TIMING_ALL      0
 #define DG_TIMING_DOMINANT 1
 int dg_encode_plan_set_timing(dg_encode_plan_t *plan, int slots);
 int dg_encode_plan_set_timing_mode(dg_encode_plan_t *plan, int mode);
+int dg_encode_plan_set_timing_every(dg_encode_plan_t *plan, int every);
 int dg_encode_plan_stage_times(dg_encode_plan_t *plan, float *ms,
                                const char **names, int n);
 /* --verbose counters (correcting plans): d_stats = 8 u64 per pair in device
@@ -354,9 +358,8 @@ int dg_decode_batch_device(dg_context_t *ctx, const uint8_t *d_ref,
  * header) and checks both against the header.  Status precedence per
  * stream: DG_ERR_MALFORMED / DG_ERR_CAPACITY, then DG_ERR_SRC_CRC, then
  * DG_ERR_DST_CRC (main.c:335-385).  Arena base pointers d_ref and d_out must
- * be 16-byte aligned.  Timing as for the encode plan; stage names "ref_crc",
- * "decode", "out_crc+verify", "total" ("decode" covers the CRC checks, the
- * two CRC stages are empty). */
+ * be 16-byte aligned.  Timing as for the encode plan, with one stage,
+ * "decode" (the kernel, CRC checks included). */
 typedef struct dg_decode_plan dg_decode_plan_t;
 int dg_decode_plan_create(dg_context_t *ctx, const dg_decode_desc_t *descs,
                           uint32_t n, int ignore_hash,
@@ -365,6 +368,7 @@ int dg_decode_plan_run(dg_decode_plan_t *plan, const uint8_t *d_ref,
                        const uint8_t *d_delta, uint8_t *d_out,
                        uint64_t *d_out_len, int32_t *d_status, void *stream);
 int dg_decode_plan_set_timing(dg_decode_plan_t *plan, int slots);
+int dg_decode_plan_set_timing_every(dg_decode_plan_t *plan, int every);
 int dg_decode_plan_stage_times(dg_decode_plan_t *plan, float *ms,
                                const char **names, int n);
 void dg_decode_plan_destroy(dg_decode_plan_t *plan);

@@ -27,6 +27,7 @@ def main():
     args.no_cpu_baseline = True
     # "dominant" (bench.py's default), "all" stage events or "none" in the timed steps
     args.stage_timing = os.environ.get("AB_TIMING", "dominant")
+    args.timing_every = int(os.environ.get("AB_EVERY", bench.TIMING_EVERY))   # timed steps with events
     import torch
     torch.cuda.set_device(0)
     R = bench.Rank(1, 0, 0, None, torch)

@@ -73,3 +73,21 @@ def test_compact_line_fits_driver_tail():
     assert d["cpu_baseline"]["cores"] and d["cpu_baseline"]["kind"] == "reference"
     assert set(d["also"]) == set(names)
     assert all("value" in e and "frac" in e for e in d["also"].values())
+
+
+@pytest.mark.parametrize("steps,warmup", [(1, 0), (2, 1), (3, 5), (5, 2), (100, 20), (101, 0)])
+def test_timing_ring_holds_only_timed_steps(steps, warmup):
+    """bench.py records the kernel events on every `every`-th step after
+    set_timing (the first, then every k-th, warmup steps included); the ring
+    of `slots` recorded runs must lie inside the K timed steps and not be
+    empty (plain simulation of dg_*_plan_set_timing_every)."""
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+    finally:
+        sys.path.remove(ROOT)
+    every, slots = bench.timing_ring(steps)
+    recorded = [i for i in range(warmup + steps) if i % every == 0]
+    ring = recorded[-slots:]
+    assert ring and all(i >= warmup for i in ring), (every, slots, ring)
+    assert every <= bench.TIMING_EVERY
