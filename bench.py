@@ -237,8 +237,25 @@ def cpu_baseline(name):
         "single_thread": {"value": round(one["gib_per_s"], 4), "pairs": n1,
                           "median_s": one.get("median_s"), "times_s": one.get("times_s")},
         "nproc": os.cpu_count(),
+        "affinity_cpus": _affinity(),
+        "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+        # the GPU pool grants each one-GPU lease a share of the host (16 CPUs,
+        # OMP_NUM_THREADS=16) while nproc shows the whole machine: the timed
+        # baseline stays inside the share; beside it, the single-thread rate
+        # scaled linearly to every host CPU (an upper bound: the reference's
+        # malloc-bound chain scales sub-linearly)
+        "full_host_upper_bound": {"value": round(one["gib_per_s"] * (os.cpu_count() or 1), 4),
+                                  "cores": os.cpu_count(),
+                                  "basis": "single_thread x nproc (not run: outside the lease's CPU share)"},
         "cpu_model": cpu_model(),
     }
+
+
+def _affinity():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return None
 
 
 # ───────────────────────────── device workloads ─────────────────────────────
@@ -767,6 +784,11 @@ def _cpu_short(cb):
     out["sample"] = smp.split(" (times")[0][:220]
     if cb.get("single_thread"):
         out["single_thread"] = cb["single_thread"]["value"]
+    for k in ("nproc", "affinity_cpus"):
+        if cb.get(k) is not None:
+            out[k] = cb[k]
+    if cb.get("full_host_upper_bound"):
+        out["full_host_upper_bound"] = cb["full_host_upper_bound"]["value"]
     return out
 
 
@@ -784,6 +806,8 @@ def _roof_short(r):
 def also_entry(line):
     """One config of the run in a few numbers (the full line is in the file)."""
     if "roofline" not in line:   # the host-to-host line (bench_e2e)
+        if line.get("error"):
+            return {"value": None, "error": line["error"], "metric": "e2e"}
         return {"value": line["value"], "ms_per_call": line["ms_per_call"], "h2d_gibs": line["h2d_gibs"],
                 "metric": "e2e"}
     r = line["roofline"]
@@ -953,8 +977,14 @@ def main():
         also[name] = measure()
     if release:
         release()
-    if args.e2e and world == 1:
-        also["e2e_c2"] = bench_e2e(args, R, dg, ctx, stream)
+    if args.e2e and world == 1 and args.config == "c2":
+        # (only beside the C2 headline, and a box without the
+        # pinned memory reports the failure in the line instead of aborting)
+        try:
+            also["e2e_c2"] = bench_e2e(args, R, dg, ctx, stream)
+        except Exception as e:  # noqa: BLE001
+            torch.cuda.synchronize()
+            also["e2e_c2"] = {"value": None, "error": f"{type(e).__name__}: {e}"[:200]}
     add_cpu_baseline(args.config, line, args, R)
     for name in extras:
         add_cpu_baseline(name, also[name], args, R)

@@ -365,6 +365,7 @@ int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algo
 	// the device failed keeps its own status) at the bytes written so far
 	uint64_t pos = 0;
 	int rc_all = DG_OK;
+	int rc_hard = DG_OK;   // the first range that failed as a whole (HIP, NOMEM, ...)
 	bool full = false;
 	out_offsets[0] = 0;
 	for (uint32_t d = 0; d < D; ++d) {
@@ -375,7 +376,7 @@ int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algo
 				out_offsets[r.lo + k + 1] = pos;
 				if (status) status[r.lo + k] = r.rc;
 			}
-			if (rc_all == DG_OK) rc_all = r.rc;
+			if (rc_hard == DG_OK) rc_hard = r.rc;
 			continue;
 		}
 		uint32_t fit = 0;   // this range's leading pairs that fit
@@ -396,9 +397,21 @@ int dg_encode_pipelined_multi(dg_context_t* const* ctxs, uint32_t n_ctx, dg_algo
 		}
 		pos += r.off[fit];
 	}
+	// as the one-device path: a hard failure wins over capacity and over the
+	// per-pair status array
+	if (rc_hard != DG_OK) return rc_hard;
 	if (full) return DG_ERR_CAPACITY;
 	return status ? DG_OK : rc_all;
 }
+
+namespace {
+// restores the calling thread's current device on every return
+struct DeviceGuard {
+	int dev = -1;
+	DeviceGuard() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+	~DeviceGuard() { if (dev >= 0) (void)hipSetDevice(dev); }
+};
+}  // namespace
 
 int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h_ref, const uint8_t* h_ver,
                         const dg_pair_t* pairs, uint32_t n, const dg_diff_options_t* opts,
@@ -409,7 +422,9 @@ int dg_encode_pipelined(dg_context_t* ctx, dg_algorithm_t algo, const uint8_t* h
 	if (n == 0) return DG_OK;
 	if (opts && ((opts->flags >> DG_OPT_INPLACE) & 1)) return DG_ERR_UNSUPPORTED;   // host step: dg_encode_batch
 	// the calling thread's current device becomes the context's before any
-	// stream or event of it is made (a new host thread starts on device 0)
+	// stream or event of it is made (a new host thread starts on device 0),
+	// and is the caller's again on return
+	DeviceGuard keep_device;
 	if (hipSetDevice(dg::ctx_device(ctx)) != hipSuccess) return DG_ERR_HIP;
 	dg_diff_options_t o;
 	if (opts) o = *opts; else dg_diff_options_default(&o);

@@ -33,8 +33,8 @@
 //                     (slot -> earliest step) entries into a per-pair table in
 //                     HBM under a per-epoch tag (never cleared).
 // Bytes come from per-wave LDS windows over V and R (p = 16, 16-byte aligned
-// pairs): both cursors only move forward within a pair, so a 4 KiB window per
-// stream is refilled by LDS-DMA every few dozen epochs instead of paying two
+// pairs): both cursors only move forward within a pair, so a 3 KiB window per
+// stream (kWin) is refilled by LDS-DMA every few dozen epochs instead of paying two
 // dependent HBM round trips per epoch.  Other seed lengths / unaligned pairs
 // read HBM/L2 directly.
 //

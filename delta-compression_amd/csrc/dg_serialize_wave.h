@@ -179,11 +179,23 @@ struct RecWords {   // the record arrays: W words per record, ADD head in the 4t
 // the records' use (placed after this tile's stores, uncountable across the
 // loop) waited for every store to land; serialize_wave_kernel 40.1 -> 35.7 us
 // at C2 (profiles/r05_experiments.md).  The wait holds the registers ("+v"),
-// so nothing reads them before it.
-__device__ __forceinline__ uint32_t rec_load(const uint32_t* p) {
-	uint32_t v;
-	asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-	return v;
+// so nothing reads them before it.  The four loads are one asm block ending in
+// `s_nop 5`, the wait is `s_nop 4` + `s_waitcnt vmcnt(N)`: markers by which
+// tests/test_isa_serialize.py finds both in the built code object and checks,
+// over every control-flow path between them, that N is covered by the VMEM
+// operations issued after the loads and that nothing touches their registers
+// before the wait.
+__device__ __forceinline__ void rec_load4(const uint32_t* p, const uint32_t* p3, uint32_t& a, uint32_t& b,
+                                          uint32_t& c, uint32_t& d) {
+	asm volatile(
+	    "global_load_dword %0, %4, off\n\t"
+	    "global_load_dword %1, %4, off offset:4\n\t"
+	    "global_load_dword %2, %4, off offset:8\n\t"
+	    "global_load_dword %3, %5, off\n\t"
+	    "s_nop 5"
+	    : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+	    : "v"(p), "v"(p3)
+	    : "memory");
 }
 
 template <uint32_t kStageBytes, int kCmd, class Src>
@@ -199,18 +211,19 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 	constexpr uint32_t kTileStores = kStageBytes / 256 + 2;   // head bytes, dwords, tail bytes
 	static_assert(kTileStores <= 63, "vmcnt holds 6 bits");
 	constexpr bool kAsm = !Src::kAlwaysHead;
-	auto load_tile = [&](uint32_t t) {   // records t + lane (clamped: every lane loads)
+	// Records t + lane, clamped to the last record (n >= 1): every lane loads,
+	// unconditionally, so the destination registers have no merge point the
+	// compiler could copy them across before the hand-counted wait.  The 4th
+	// word comes from word 2 when W < 4 (never read then: inl() is false).
+	auto load_tile = [&](uint32_t t) {
 		const uint32_t j = umin32(t + lane, n - 1);
 		const uint32_t* r = src.rec + (uint64_t)src.W * j;
-		ncv[0] = rec_load(r);
-		ncr[0] = rec_load(r + 1);
-		ncl[0] = rec_load(r + 2);
-		ncw[0] = src.W >= 4 ? rec_load(r + 3) : 0u;
+		rec_load4(r, r + (src.W >= 4 ? 3 : 2), ncv[0], ncr[0], ncl[0], ncw[0]);
 	};
 	if constexpr (kAsm) {
-		ncv[0] = ncr[0] = ncl[0] = ncw[0] = 0;
-		if (n) load_tile(0);
-		asm volatile("s_waitcnt vmcnt(0)" : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])::"memory");
+		if (n == 0) return 0;
+		load_tile(0);
+		asm volatile("s_nop 4\n\ts_waitcnt vmcnt(0)" : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])::"memory");
 	} else
 #pragma unroll
 	for (int i = 0; i < kCmd; ++i) {
@@ -234,9 +247,7 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 			ncv[i] = ncr[i] = ncl[i] = ncw[i] = 0;
 			if (jn < n) src.load(jn, ncv[i], ncr[i], ncl[i], ncw[i]);
 		}
-		if constexpr (kAsm) {
-			if (t0 + 64 < n) load_tile(t0 + 64);
-		}
+		if constexpr (kAsm) load_tile(t0 + 64);   // past the end: record n - 1 again (not used)
 		// the lane's last valid command end, and the lane's byte count
 		uint32_t last = 0, sz = 0;
 #pragma unroll
@@ -301,7 +312,7 @@ __device__ inline uint64_t serialize_run(uint8_t* out, const uint8_t* V, uint32_
 		// buffer stores (a tile past the stage drained its stores with
 		// vmcnt(0)), so vmcnt(kTileStores) covers them and no store
 		if constexpr (kAsm)
-			asm volatile("s_waitcnt vmcnt(%4)"
+			asm volatile("s_nop 4\n\ts_waitcnt vmcnt(%4)"
 			             : "+v"(ncv[0]), "+v"(ncr[0]), "+v"(ncl[0]), "+v"(ncw[0])
 			             : "n"(kTileStores)
 			             : "memory");

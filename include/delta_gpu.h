@@ -287,8 +287,11 @@ int dg_encode_pipelined(dg_context_t *ctx, dg_algorithm_t algo,
  * status) with out_offsets at the bytes written (the one-device call stops
  * at a chunk boundary instead).  No bytes move between devices.  n_ctx == 1
  * is dg_encode_pipelined.  Returns as dg_encode_pipelined (the first failing
- * range's code when status is NULL).  The multi-device path has only run
- * with several contexts on one device (tests/test_gpu_pipelined.py). */
+ * range's code when status is NULL; a range that failed as a whole returns
+ * its code even when status is given).  UNVERIFIED on two or more physical
+ * devices: the multi-device path has only run with several contexts on one
+ * device (tests/test_gpu_pipelined.py); the caller's current device is
+ * restored on return. */
 int dg_encode_pipelined_multi(dg_context_t *const *ctxs, uint32_t n_ctx, dg_algorithm_t algo,
                               const uint8_t *h_ref, const uint8_t *h_ver,
                               const dg_pair_t *pairs, uint32_t n_pairs,

@@ -163,3 +163,45 @@ def test_pipelined_multi_tight_capacity(dg, orc):
         exp.append(exp[-1] + len(w))
     assert list(offs) == exp + [written] * (n - first)
     assert bytes(ho[:written]) == b"".join(want[:first])
+
+
+def test_pipelined_multi_range_failure_wins_over_status(dg, orc):
+    """a range that fails as a whole (here: plan creation refuses a
+    pair of >= 4 GiB, DG_ERR_TOO_LARGE, before any byte is read) makes the
+    multi-device call return that code even when a status array is passed, as
+    the one-device call does; its pairs carry the code, the other range's
+    pairs are written and DG_OK.  The caller's current device is unchanged."""
+    import ctypes as C
+    import torch
+    L = dg._lib
+    n = 6
+    pairs = [(bytes((5 * k + i) & 0xFF for k in range(4096)),) * 2 for i in range(n)]
+    pairs = [(R, R[:100] + bytes(16) + R[116:]) for (R, _) in pairs]
+    want = [orc.encode(ONEPASS, R, V, p=16, q=97) for R, V in pairs]
+    huge = n - 2   # R of 5 GiB (never read: the plan refuses it first)
+    lay = [(i * 4096, 4096, i * 4096, 4096) for i in range(n)]
+    lay[huge] = (0, 5 << 30, huge * 4096, 4096)
+    hr = (C.c_uint8 * (n * 4096)).from_buffer_copy(b"".join(R for R, _ in pairs))
+    hv = (C.c_uint8 * (n * 4096)).from_buffer_copy(b"".join(V for _, V in pairs))
+    cap = 1 << 20
+    ho = (C.c_uint8 * cap)()
+    pa = (L.Pair * n)(*[L.Pair(*x) for x in lay])
+    offs = (C.c_uint64 * (n + 1))(*([12345] * (n + 1)))
+    st = (C.c_int32 * n)(*([0] * n))
+    o = L.DiffOptions.make(q=97)
+    ctxs = [dg.Context(0) for _ in range(2)]
+    dev0 = torch.cuda.current_device()
+    try:
+        hs = (C.c_void_p * 2)(*[c.handle for c in ctxs])
+        rc = dg.lib.dg_encode_pipelined_multi(hs, 2, ONEPASS, C.addressof(hr), C.addressof(hv), pa, n, C.byref(o),
+                                              1 << 20, C.addressof(ho), cap, offs, st)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert rc == 3   # DG_ERR_TOO_LARGE
+    assert torch.cuda.current_device() == dev0
+    assert list(st[:huge]) == [0] * huge
+    assert all(s == 3 for s in st[huge:])
+    written = sum(len(w) for w in want[:huge])
+    assert bytes(ho[:written]) == b"".join(want[:huge])
+    assert offs[huge] == written
