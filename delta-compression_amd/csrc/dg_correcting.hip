@@ -87,6 +87,24 @@ __device__ __forceinline__ uint64_t roll61w(uint64_t fp, uint64_t nb, uint32_t i
 	return ((uint64_t)rh << 32) | rl;
 }
 
+// roll61w with the leaving byte's term computed instead of looked up: x *
+// cneg == -x 263^p (mod M) for cneg = M - 263^p mod M, split into its dwords
+// (x cneg_lo < 2^40, x cneg_hi < 2^37), so P < 2^41 and Q < 2^39 and the same
+// fold applies.  Two more multiply-adds per step, and no LDS read (with its
+// wait, which also waited for the slot atomics issued before it) on the
+// rolling chain.
+__device__ __forceinline__ uint64_t roll61x(uint64_t fp, uint32_t x, uint32_t cneg_lo, uint32_t cneg_hi, uint32_t in) {
+	const uint64_t P = (uint64_t)(uint32_t)fp * (uint32_t)kBase + (uint64_t)x * cneg_lo;
+	const uint64_t Q = (uint64_t)(uint32_t)(fp >> 32) * (uint32_t)kBase + (uint64_t)x * cneg_hi;
+	const uint32_t s = (uint32_t)(Q >> 29) + in;
+	const uint32_t tl = (uint32_t)P + s;
+	const uint32_t th = (uint32_t)(P >> 32) + ((uint32_t)Q & 0x1FFFFFFFu) + (tl < s ? 1u : 0u);
+	const uint32_t f = th >> 29;
+	const uint32_t rl = tl + f;
+	const uint32_t rh = (th & 0x1FFFFFFFu) + (rl < f ? 1u : 0u);
+	return ((uint64_t)rh << 32) | rl;
+}
+
 // r <= M + 2 to [0, M): r - M = r + 1 - 2^61 leaves only the low dword + 1
 __device__ __forceinline__ uint64_t fp61_canon(uint64_t r) {
 	const bool ge = r >= kMersenne;
@@ -401,6 +419,9 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 // raw CRC of R followed by pad = 32 Ki * iterations - |R| zero bytes; the
 // plan's per-pair x^(-8 pad) removes them.  init = ~0 is the first 8 bytes
 // XOR-ed with 0xFF (lane 0, iteration 0), xorout the final inversion.
+#ifndef DG_CORR_NB_LDS   // 0 (A/B): the leaving byte's term computed (roll61x), measured 1-2 % slower
+#define DG_CORR_NB_LDS 1
+#endif
 constexpr uint32_t kBuildLdsBlock = 1024;
 constexpr uint32_t kCrcPiece = kBuildSeedsPerLane;                    // bytes per lane per iteration
 constexpr uint32_t kCrcStride = kBuildLdsBlock * kBuildSeedsPerLane;  // 32 KiB per iteration
@@ -420,6 +441,12 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 	uint32_t* H = a.ctab + pp.tab_base;
 	for (uint32_t i = tid; i < cap; i += kBuildLdsBlock) T[i] = kNone;
 	if (tid < 256) nb[tid] = roll_table(tid, a.powc[0]);
+	// -263^p mod M as dwords (roll61x); uniform
+	[[maybe_unused]] const uint64_t cneg = [&] {
+		const uint64_t v = mulsmall61(a.powc[0], (uint32_t)kBase);
+		return v ? kMersenne - v : 0ull;
+	}();
+	[[maybe_unused]] const uint32_t cneg_lo = (uint32_t)cneg, cneg_hi = (uint32_t)(cneg >> 32);
 	if constexpr (CRC) {
 		for (uint32_t i = tid; i < 4 * 256; i += kBuildLdsBlock) CT[i] = a.crc_tab[i];
 		if (tid < 256) CT[4 * 256 + tid] = a.crc_tab[8 * 256 + 5 * kCrcNibTabWords + tid];   // level 5: x^(8*32 Ki)
@@ -496,8 +523,13 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 #pragma unroll
 					for (uint32_t j = 0; j < kBuildSeedsPerLane / 2; ++j) {
 						if (j) {   // roll (hash.c:62-98), weakly reduced
+#if DG_CORR_NB_LDS
 							fa = roll61w(fa, nb[byte_at(j - 1)], byte_at(j + 15));
 							fb = roll61w(fb, nb[byte_at(j + 15)], byte_at(j + 31));
+#else
+							fa = roll61x(fa, byte_at(j - 1), cneg_lo, cneg_hi, byte_at(j + 15));
+							fb = roll61x(fb, byte_at(j + 15), cneg_lo, cneg_hi, byte_at(j + 31));
+#endif
 						}
 						// a weakly reduced value >= M is ~2^-60 likely: one
 						// compare per seed, the subtract only in a wave that has one

@@ -210,6 +210,19 @@ constexpr uint32_t kBloomBase = DG_BLOOM_BASE;
 #define DG_BACKOFF_MAX 4
 #endif
 constexpr uint32_t kBackoffMax = DG_BACKOFF_MAX;   // tier backoff: at most 2^k - 1 epochs skipped
+#ifndef DG_DIAG_WINLIM
+#define DG_DIAG_WINLIM 0
+#endif
+#ifndef DG_DIAG_MINSCAN
+#define DG_DIAG_MINSCAN 512
+#endif
+#ifndef DG_REFILL_TOUCH
+#define DG_REFILL_TOUCH 0
+#endif
+constexpr uint32_t kTouchAhead = DG_REFILL_TOUCH;   // bytes past a refilled window warmed in the caches
+static_assert(kTouchAhead % 128 == 0 && kTouchAhead <= 8192, "one lane per 128-byte line");
+constexpr bool kDiagWinLim = DG_DIAG_WINLIM != 0;    // diagonal batch scans what the windows hold first
+constexpr uint32_t kDiagMinScan = DG_DIAG_MINSCAN;  // ... when that is at least this many bytes
 
 // p = 16 and 16-byte aligned stream bases: sliding LDS windows.
 struct WinSrc {
@@ -219,6 +232,7 @@ struct WinSrc {
 	uint32_t len[2];
 	uint32_t base[2];        // stream offset held at win[s][0], multiple of 16
 	lds_u8* win;             // LDS (address space 3), 2 x kWinStride
+	lds_u8* touch;           // DG_REFILL_TOUCH: 256 bytes of LDS the cache-warming DMA lands in
 	const uint64_t* powc;
 	// Mismatch list of the diagonal batch (LDS, u16 offsets from lc_base,
 	// ascending; the stream end counts as one), made afresh by every call.
@@ -275,6 +289,23 @@ struct WinSrc {
 		refill_cycles += __builtin_amdgcn_s_memtime() - tr0;
 		++refill_count;
 #endif
+		if constexpr (kTouchAhead > 0) {
+			// warm the caches for the next refill: one dword per 128-byte line
+			// of the kTouchAhead bytes past each refilled window, by LDS-DMA into
+			// a dummy area (nothing waits for it: the next refill's own loads are
+			// issued after it, and vmcnt drains in order)
+			const uint32_t lanes = kTouchAhead / 128;
+			if (lane < lanes) {
+				if (fv) {
+					const uint32_t off = base[0] + kWin + 128 * lane;
+					if (off < len[0]) __builtin_amdgcn_global_load_lds((const void*)(S[0] + off), (lds_void_t*)touch, 4, 0, 0);
+				}
+				if (fr) {
+					const uint32_t off = base[1] + kWin + 128 * lane;
+					if (off < len[1]) __builtin_amdgcn_global_load_lds((const void*)(S[1] + off), (lds_void_t*)touch, 4, 0, 0);
+				}
+			}
+		}
 		PROF_ADD(*this, P_REFILLS, 1);
 		PROF_ADD(*this, P_T_REFILL, PROF_NOW_R() - t0);
 	}
@@ -353,24 +384,43 @@ struct WinSrc {
 	// value so nothing goes through scratch): the number committed, adv =
 	// offset of the new state, more = the batch ended only because the chain
 	// left the known region (another batch can follow directly), dadd = their
-	// delta bytes, long_first = nothing was committed because the first
+	// delta bytes, long_first = 1: nothing was committed because the first
 	// epoch's diagonal step is past 63 (phase A cannot resolve it on the
-	// diagonal: the caller starts phase B at step 0).
+	// diagonal: the caller starts phase B at step 0); 2: a scan truncated to
+	// the windows found no member (the caller runs the batch again in full).
 	struct DiagOut {
 		uint32_t committed, adv, more, dadd, long_first;
 	};
 	__device__ DiagOut diag_batch(uint32_t v0, uint32_t r0, uint32_t vl, uint32_t rl, uint64_t q,
 	                              uint64_t qmag, const ModQ& mq, uint32_t p, uint32_t* rec, uint32_t nrec,
-	                              uint32_t rec_cap, uint32_t* mlist) {
+	                              uint32_t rec_cap, uint32_t* mlist, bool full_scan) {
 		const uint32_t lane = lane_id();
 		const uint32_t lim = umin32(vl - v0, rl - r0);
 		if (lim < p + 1) return DiagOut{0, 0, 0, 0, 0};
 		[[maybe_unused]] uint64_t tq = PROF_NOW();
-		// 1. the list of mismatch offsets from v0
-		ensure2(v0, r0, 64 * kLook + 48, true, true);
+		// 1. the list of mismatch offsets from v0, over `scan` bytes.  With
+		// DG_DIAG_WINLIM the batch first scans only what both windows already
+		// hold from (v0, r0) when that is at least kDiagMinScan bytes, so a
+		// window is refilled when the chain nears its end instead of whenever
+		// less than the full look-ahead is left (fewer refills, less overlap
+		// re-read); a truncated scan that yields no member returns long_first
+		// = 2 and the caller runs the batch again in full (full_scan).
+		uint32_t scan = 64 * kLook;
+		bool trunc = false;
+		if (kDiagWinLim && !full_scan) {
+			const uint32_t hv = v0 - base[0] < kWin ? base[0] + kWin - v0 : 0u;
+			const uint32_t hr = r0 - base[1] < kWin ? base[1] + kWin - r0 : 0u;
+			const uint32_t have = umin32(hv, hr);
+			if (have < 64 * kLook + 48 && have >= kDiagMinScan + 48) {
+				scan = (have - 48) & ~(kLook - 1u);
+				trunc = true;
+			}
+		}
+		if (!trunc) ensure2(v0, r0, 64 * kLook + 48, true, true);
 		{
 			// mismatch bits of offsets [kLook*lane, kLook*lane + kLook)
 			const uint32_t base = kLook * lane;
+			const bool inscan = base < scan;   // (scan is a multiple of kLook)
 			// The lane's 32 bytes of each stream come in as three ds_read_b128 from
 			// the 16-byte-aligned address below them (2-way bank conflicts; word
 			// reads at a 32-byte lane stride are 8-way).  The offset inside the
@@ -378,8 +428,8 @@ struct WinSrc {
 			// so picking the 8 words is a uniform switch plus alignbytes.
 			static_assert(kLook == 32, "one 32-bit mask per lane, 16-byte-aligned lane chunks");
 			uint32_t wv[8], wr[8];
-			lane_words32(0, v0 + base, wv);
-			lane_words32(1, r0 + base, wr);
+			lane_words32(0, v0 + (inscan ? base : 0u), wv);
+			lane_words32(1, r0 + (inscan ? base : 0u), wr);
 			// byte j of word g first lands at bit 8j + g (one shift-and-or per
 			// word), then a 5-bit index rotation (four delta swaps) moves it to
 			// bit 4g + j, i.e. offset order
@@ -391,7 +441,9 @@ struct WinSrc {
 				bits |= (t >> (7 - g)) & (0x01010101u << g);
 			}
 			bits = mask_transpose_8x4(bits);
-			if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
+			if (!inscan) {
+				bits = 0u;   // not scanned: unknown, not a terminator
+			} else if (base + kLook > lim) {   // past the shorter stream: only its end terminates a match
 				bits = lim > base ? (bits & ((1u << (lim - base)) - 1u)) : 0u;
 				if (lim >= base && lim < base + kLook) bits |= 1u << (lim - base);
 			}
@@ -407,7 +459,7 @@ struct WinSrc {
 			__builtin_amdgcn_wave_barrier();
 		}
 		const uint32_t K = umin32(lc_n, 64u);
-		if (K < 2) return DiagOut{0, 0, 0, 0, 0};
+		if (K < 2) return DiagOut{0, 0, 0, 0, trunc ? 2u : 0u};
 		{
 			// the window must hold every byte the batch's steps read
 			const uint32_t last = (uint32_t)lc[K - 1];
@@ -433,7 +485,7 @@ struct WinSrc {
 		const bool cand = gap && lane < kb;        // members, in chain order
 		const uint32_t Bend = wave_incl_scan(cand ? T + 1 : 0u);   // steps through this member
 		uint64_t left = __ballot(cand);
-		if (!left) return DiagOut{0, 0, 0, 0, tooLong != 0 ? 1u : 0u};
+		if (!left) return DiagOut{0, 0, 0, 0, tooLong != 0 ? 1u : (trunc ? 2u : 0u)};
 		PROF_ADD(*this, P_T_D2, PROF_NOW() - tq);
 		// Members are taken in rounds of at most 64 steps (a member never
 		// straddles two rounds); the first member that fails its check ends
@@ -693,6 +745,7 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 	// 2^k - 1 epochs go straight to the next tier (the result is the same, the
 	// tiers only differ in cost)
 	uint32_t diag_miss = 0, diag_skip = 0, a_miss = 0, a_skip = 0;
+	bool diag_full = false;   // the next diagonal batch scans its full look-ahead
 
 	// ── member mode (dg_members.hip): verified diagonal members are taken as
 	//    they are, 64 records per pass, chunk after chunk; the epochs below
@@ -853,7 +906,9 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 			if (try_diag) {
 				[[maybe_unused]] const uint64_t td = PROF_NOW();
 				if (members) nb_note();
-				const auto dg = src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm);
+				const auto dg = src.diag_batch(v0, r0, vl, rl, q, qmag, mq, p, rec, nrec, rec_cap, bm, diag_full);
+				diag_full = false;
+				if (uni(dg.long_first) == 2u) { diag_full = true; continue; }   // the same state, scanned in full
 				const uint32_t f = uni(dg.committed);
 				skipA = f == 0 && uni(dg.long_first) != 0u;
 				// matches that leave the diagonal (insertions, deletions, moved
@@ -1264,6 +1319,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	__shared__ __attribute__((aligned(16))) uint8_t win[2 * kWinStride];
 	__shared__ uint32_t bm[256];   // phase-B bitmaps / batch scratch, member table, round bitmaps
 	__shared__ __attribute__((aligned(4))) uint16_t lcache[kListCap];   // the diagonal batch's mismatch list; phase-C chunk bitmaps
+	__shared__ __attribute__((aligned(16))) uint8_t touch[kTouchAhead > 0 ? 256 : 4];
 	const uint32_t pair = a.pair0 + blockIdx.x;
 	if (pair >= a.n_pairs) return;
 	const PairDev pd = a.pairs[pair];
@@ -1288,6 +1344,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	src.len[1] = (uint32_t)pd.r_len;
 	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
 	src.win = (lds_u8*)win;
+	src.touch = (lds_u8*)touch;
 	src.lc = lcache;
 	src.powc = a.powc;
 	PROF_INIT(src)

@@ -98,21 +98,22 @@ __device__ __forceinline__ void put_cmds(P base, const bool (&valid)[kCmd], uint
 				if (inl && gap <= 4) {   // payload carried in the record
 					for (uint32_t k = 0; k < gap; ++k) q[9 + k] = (uint8_t)(cw[i] >> (8 * k));
 				} else if (gap <= 32) {
-					// up to 8 (unaligned) dword loads in flight instead of a
-					// chain of byte loads; never past the end of V
+					// 8 unaligned dword loads, all issued unconditionally (a
+					// per-word condition made the compiler branch around each
+					// load and wait for it, and for every store before it: up to
+					// 8 dependent round trips per tile), at addresses clamped
+					// inside V (gap > 4 and prev + gap <= |V|, so |V| >= 5); a
+					// word that crosses |V| is loaded from |V| - 4 and shifted
+					// down, a word past |V| is never used
 					uint32_t wd[8];
+					const uint32_t vl4 = vl - 4u;
 #pragma unroll
 					for (int k = 0; k < 8; ++k) {
-						const uint32_t o4 = 4u * k;
-						wd[k] = 0;
-						if (o4 < gap) {
-							if (prev + o4 + 4 <= vl) {
-								__builtin_memcpy(&wd[k], V + prev + o4, 4);
-							} else {
-								for (uint32_t b = 0; b < 4 && prev + o4 + b < vl; ++b)
-									wd[k] |= (uint32_t)V[prev + o4 + b] << (8 * b);
-							}
-						}
+						const uint32_t o4 = prev + 4u * k;
+						const uint32_t a4 = umin32(o4, vl4);
+						uint32_t w;
+						__builtin_memcpy(&w, V + a4, 4);
+						wd[k] = w >> (8u * umin32(o4 - a4, 3u));
 					}
 #pragma unroll
 					for (int k = 0; k < 32; ++k)
