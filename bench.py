@@ -166,6 +166,24 @@ def pmc_traffic(config, kernel):
     return None, (f"stale: {stale} was measured on another build of the library" if stale else None)
 
 
+def pmc_path(config):
+    """HBM bytes per step of every kernel of the step (profiles/<round>_pmc_path_
+    <config>.json, scripts/profile_round.sh path + profile_collect.py), lower and
+    upper readings, or None when the newest summary is of another library build."""
+    import glob
+    cur = lib_sha16()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_path_{config}.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("path_traffic_per_step"):
+            if d.get("lib_sha16") and d["lib_sha16"] == cur:
+                return d, os.path.relpath(f, ROOT)
+            return None, f"stale: {os.path.relpath(f, ROOT)} was measured on another build of the library"
+    return None, None
+
+
 # ───────────────────────────── CPU baseline ─────────────────────────────────
 
 def cpu_share() -> int:
@@ -522,6 +540,13 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         "cpu_baseline": None,
         "lib_sha16": lib_sha16(),
     }
+    if npg == CONFIGS[name][0]:
+        pt, pt_src = pmc_path(name)
+        rl = line["roofline"]
+        rl["path_traffic"] = pt["path_traffic_per_step"] if pt else None
+        rl["path_traffic_upper"] = pt["path_traffic_upper_per_step"] if pt else None
+        rl["path_traffic_ratio"] = round(pt["path_traffic_per_step"] / path_bytes, 3) if pt else None
+        rl["path_traffic_source"] = pt_src
     if algo == "correcting" and stages.get("corr_build") is not None:
         # the build and the scan apart (HIP events on the run stream; the
         # CRC shares the CUs with them)
@@ -794,7 +819,7 @@ def _cpu_short(cb):
 
 def _roof_short(r):
     keys = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "avg_launch_ms",
-            "algorithmic_bytes_per_launch", "path_achieved", "path_frac")
+            "algorithmic_bytes_per_launch", "path_achieved", "path_frac", "path_traffic", "path_traffic_ratio")
     out = {k: r[k] for k in keys if k in r}
     if r.get("traffic") and r.get("algorithmic_bytes_per_launch"):
         out["traffic_ratio"] = round(r["traffic"] / r["algorithmic_bytes_per_launch"], 3)
@@ -813,6 +838,8 @@ def also_entry(line):
     r = line["roofline"]
     e = {"value": line["value"], "ms_per_step": line["ms_per_step"], "kernel_ms": r.get("avg_launch_ms"),
          "frac": r.get("frac"), "path_frac": r.get("path_frac")}
+    if r.get("path_traffic_ratio"):
+        e["path_traffic_ratio"] = r["path_traffic_ratio"]
     if r.get("traffic") and r.get("algorithmic_bytes_per_launch"):
         e["traffic_ratio"] = round(r["traffic"] / r["algorithmic_bytes_per_launch"], 3)
     cb = line.get("cpu_baseline")

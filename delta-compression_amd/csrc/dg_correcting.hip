@@ -419,6 +419,11 @@ __global__ __launch_bounds__(kBuildBlock) void correcting_build_kernel(EncodeArg
 // raw CRC of R followed by pad = 32 Ki * iterations - |R| zero bytes; the
 // plan's per-pair x^(-8 pad) removes them.  init = ~0 is the first 8 bytes
 // XOR-ed with 0xFF (lane 0, iteration 0), xorout the final inversion.
+#ifndef DG_CORR_CHAINS   // rolling chains per lane in the LDS build (2 or 4)
+#define DG_CORR_CHAINS 2
+#endif
+constexpr uint32_t kCorrChains = DG_CORR_CHAINS;
+static_assert(kCorrChains == 2 || kCorrChains == 4, "chains per lane");
 #ifndef DG_CORR_NB_LDS   // 0 (A/B): the leaving byte's term computed (roll61x), measured 1-2 % slower
 #define DG_CORR_NB_LDS 1
 #endif
@@ -517,6 +522,28 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 						w[11] >>= 8;
 					}
 					auto byte_at = [&](uint32_t i) -> uint32_t { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+					if constexpr (kCorrChains == 4) {
+						// four independent rolling chains (seeds 0..7, 8..15,
+						// 16..23, 24..31): two more direct fingerprints per piece,
+						// half the dependent rolls per chain
+						uint64_t f[4];
+#pragma unroll
+						for (uint32_t c = 0; c < 4; ++c) f[c] = fp16_dot(w[2 * c], w[2 * c + 1], w[2 * c + 2], w[2 * c + 3]);
+#pragma unroll
+						for (uint32_t j = 0; j < kBuildSeedsPerLane / 4; ++j) {
+							if (j) {
+#pragma unroll
+								for (uint32_t c = 0; c < 4; ++c)
+									f[c] = roll61w(f[c], nb[byte_at(8 * c + j - 1)], byte_at(8 * c + j + 15));
+							}
+							if (__ballot(f[0] >= kMersenne || f[1] >= kMersenne || f[2] >= kMersenne || f[3] >= kMersenne)) {
+#pragma unroll
+								for (uint32_t c = 0; c < 4; ++c) f[c] = fp61_canon(f[c]);
+							}
+#pragma unroll
+							for (uint32_t c = 0; c < 4; ++c) insert(f[c], (uint32_t)(s0 + 8 * c + j));
+						}
+					} else {
 					// two independent rolling chains (seeds 0..15 and 16..31)
 					uint64_t fa = fp16_dot(w[0], w[1], w[2], w[3]);
 					uint64_t fb = fp16_dot(w[4], w[5], w[6], w[7]);
@@ -539,6 +566,7 @@ __global__ __launch_bounds__(kBuildLdsBlock) void correcting_build_lds_kernel(En
 						}
 						insert(fa, (uint32_t)(s0 + j));
 						insert(fb, (uint32_t)(s0 + 16 + j));
+					}
 					}
 				} else if (cnt) {
 					uint64_t fp = window_fp<0>(R + s0, p, a.powc);

@@ -1095,6 +1095,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.kseg = ctx->kseg;
 		return a;
 	};
+#ifndef DG_CRC5_ALL   // A/B: the five-bit row pass beside the onepass kernel too
+#define DG_CRC5_ALL 0
+#endif
+	constexpr bool kCrc5All = DG_CRC5_ALL != 0;
 	auto run_crc = [&]() -> int {
 		HIPCHK(ctx, rec(0, cs));
 		const CrcArgs a = crc_args();
@@ -1113,7 +1117,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
 			// there instead of 0.71: C4 731 -> 813 GiB/s)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            P->members ? kCrcPassRows5 : kCrcPassRows, !late_fin));
+			                            P->members || kCrc5All ? kCrcPassRows5 : kCrcPassRows, !late_fin));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;

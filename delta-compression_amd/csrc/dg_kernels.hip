@@ -310,11 +310,16 @@ hipError_t launch_synth_transpose(uint8_t* ref, uint8_t* ver, const SynthSpan* s
 // per CU are in flight and their record / payload loads overlap.  The header
 // CRC bytes are left to crc_patch_kernel, so this kernel does not wait for
 // the CRC stream.
-constexpr uint32_t kSerWaveStage = 4096;
-constexpr int kSerWaveCmds = 1;   // records per lane per tile (4 measured slower: C2 +18%, C3 3.6x)
+// (one record per lane per tile: 4 measured slower, C2 +18 %, C3 3.6x)
+#ifndef DG_SER_PIPE   // A/B: 1 = the LDS-DMA pipeline (serialize_pipe, 2 KiB stage), C2 37.7 -> 74.9 us
+#define DG_SER_PIPE 0
+#endif
+constexpr bool kSerPipe = DG_SER_PIPE != 0;
+constexpr uint32_t kSerWaveStage = kSerPipe ? 2048 : 4096;   // (pipeline rings beside a 2 KiB stage: 16 waves per CU)
+constexpr uint32_t kSerWaveLds = kSerPipe ? pipe_lds_bytes<kSerWaveStage>() : kSerWaveStage + 32;
 
 __global__ __launch_bounds__(64) void serialize_wave_kernel(SerArgs s) {
-	__shared__ __attribute__((aligned(16))) uint8_t stage[kSerWaveStage + 32];
+	__shared__ __attribute__((aligned(16))) uint8_t stage[kSerWaveLds];
 	const uint32_t pair = blockIdx.x;
 	const uint64_t base = s.offsets[pair];
 	const uint64_t end = s.offsets[pair + 1];
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(64) void serialize_wave_kernel(SerArgs s) {
 	if (s.status[pair] != 0) return;
 	const PairDev pd = s.pairs[pair];
 	const PairPlanDev pp = s.pplan[pair];
-	const int32_t st = serialize_wave<kSerWaveStage, kSerWaveCmds>(s.out + base, end - base, s.ver + pd.v_off,
+	const int32_t st = serialize_wave<kSerWaveStage, kSerPipe>(s.out + base, end - base, s.ver + pd.v_off,
 	                                                 (uint32_t)pd.v_len, s.rec + (uint64_t)s.rec_words * pp.rec_base,
 	                                                 s.rec_words, s.n_rec[pair], (sw_lds8*)stage);
 	if (st != 0 && lane_id() == 0) s.status[pair] = st;

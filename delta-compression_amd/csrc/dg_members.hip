@@ -1008,7 +1008,7 @@ __device__ __forceinline__ void member_serialize(const MemSerArgs& a, uint32_t j
 						if (e.z + n != F.end - F.base && lane == 0) a.status[F.J.pair] = 12;   // DG_ERR_INTERNAL: sizes disagree
 					} else {
 						const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (F.J.rec_base + e.x), kRecWordsOnepass};
-						serialize_run<kMemSerStage, 1>(o, V, vl, src, e.y, e.w, (sw_lds8*)stage);
+						serialize_run<kMemSerStage>(o, V, vl, src, e.y, e.w, (sw_lds8*)stage);
 					}
 				}
 			}
@@ -1017,14 +1017,249 @@ __device__ __forceinline__ void member_serialize(const MemSerArgs& a, uint32_t j
 	}
 }
 
+// ── member-mode serialisation, software-pipelined (DG_MSER_PIPE, default) ──
+//
+// member_serialize waits, for every job, for the next job's loads issued
+// after this job's stores (loads and stores share the vmcnt counter, which
+// drains in issue order: the copy of the prefetched registers waits for the
+// stores too).  Here the next job's V bytes and member records go by LDS-DMA
+// into rings of two slots, its descriptors by scalar loads (lgkmcnt, not
+// vmcnt), and a job's flush is a fixed count of buffer stores, so one
+// hand-counted s_waitcnt vmcnt(kMserTileStores) at the top of the next job
+// covers its DMAs without waiting for a single store; a job that writes more
+// (a second tile, the chain's own record runs, the tail, an oversized tile)
+// drains with vmcnt(0) instead.
+constexpr uint32_t kMserPipeStage = 2048;
+constexpr uint32_t kMserTileStores = kMserPipeStage / 1024 + 2;   // head bytes, 16-byte pieces, tail bytes
+constexpr uint32_t kMserVSlot = kStage + 16;
+typedef __attribute__((address_space(4))) const uint32_t c4_u32;
+typedef __attribute__((address_space(4))) const uint64_t c4_u64;
+
+struct SerJob {   // one job's descriptors, wave-uniform (scalar loads)
+	uint32_t pair, c, n_chunks, chunk_base, vl, cnt, boff, first;
+	int32_t st;
+	uint64_t v_off, mem_base, rec_base, base, end, slot0;
+};
+
+__device__ __forceinline__ void ser_job_pair(const MemSerArgs& a, SerJob& J) {
+	static_assert(sizeof(PairDev) == 32, "pair: r_off, r_len, v_off, v_len");
+	const c4_u64* pd = (const c4_u64*)(a.pairs + J.pair);
+	const PairPlanDev* pp = a.pplan + J.pair;
+	J.v_off = pd[2];
+	J.vl = (uint32_t)pd[3];
+	J.mem_base = ((const c4_u64*)&pp->mem_base)[0];
+	J.rec_base = ((const c4_u64*)&pp->rec_base)[0];
+	J.chunk_base = ((const c4_u32*)&pp->chunk_base)[0];
+	J.n_chunks = ((const c4_u32*)&pp->n_chunks)[0];
+}
+
+__device__ __forceinline__ void ser_job_chunk(const MemSerArgs& a, SerJob& J) {
+	J.st = (int32_t)((c4_u32*)(a.status + J.pair))[0];
+	J.base = ((c4_u64*)(a.offsets + J.pair))[0];
+	J.end = ((c4_u64*)(a.offsets + J.pair))[1];
+	const c4_u32* cm = (c4_u32*)(a.cmap + 2ull * (J.chunk_base + J.c));
+	J.cnt = cm[0];
+	J.boff = cm[1];
+	J.slot0 = J.mem_base + (uint64_t)J.c * kMemChunkSlots;
+	J.first = ((c4_u32*)(a.mem_s + J.slot0))[0];
+}
+
+__device__ __forceinline__ void ser_job_start(const MemSerArgs& a, SerJob& J, uint32_t job) {
+	const c4_u32* jb = (c4_u32*)(a.chunks + job);
+	J.pair = jb[0];
+	J.c = jb[1];
+	ser_job_pair(a, J);
+	ser_job_chunk(a, J);
+}
+
+__device__ __forceinline__ void ser_job_next(const MemSerArgs& a, SerJob& J) {
+	if (J.c + 1 < J.n_chunks) {
+		++J.c;
+	} else {
+		++J.pair;
+		J.c = 0;
+		ser_job_pair(a, J);
+	}
+	ser_job_chunk(a, J);
+}
+
+// the job's V region [c * 2048 - 16, + kStage) and member records 0..63 into
+// ring slot s; pieces not wholly inside V are left out (never read, except the
+// one that straddles |V|, rebuilt after landing)
+__device__ __forceinline__ void ser_job_dma(const MemSerArgs& a, const SerJob& J, uint8_t* vslot, uint8_t* rslot) {
+	const uint32_t lane = lane_id();
+	const int64_t g0 = (int64_t)J.c * kMemChunk - 16;
+	const uint8_t* V = a.ver + J.v_off;
+#pragma unroll
+	for (uint32_t k = 0; k < kStageRows; ++k) {
+		const int64_t p = g0 + 1024 * k + 16 * lane;
+		if (1024 * k + 16 * lane < kStage && p >= 0 && p + 16 <= (int64_t)J.vl)
+			__builtin_amdgcn_global_load_lds((const void*)(V + p), (lds_void_t*)(vslot + 1024 * k), 16, 0, 0);
+	}
+	if (lane < J.cnt && lane < 64)
+		__builtin_amdgcn_global_load_lds((const void*)(a.srec + 4ull * (J.slot0 + lane)), (lds_void_t*)rslot, 16, 0, 0);
+}
+
+__device__ __forceinline__ void member_serialize_pipe(const MemSerArgs& a, uint32_t j0, uint32_t j1, uint8_t* vring,
+                                                      uint8_t* rring, uint8_t* stage) {
+	typedef __attribute__((address_space(3))) const uint32_t lds32c;
+	const uint32_t lane = lane_id();
+	SerJob F, N;
+	ser_job_start(a, F, j0);
+	ser_job_dma(a, F, vring, rring);
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	for (uint32_t j = j0, slot = 0; j < j1; ++j, slot ^= 1u) {
+		// this job's DMAs have landed: only the previous job's kMserTileStores
+		// stores were issued after them (or everything was drained)
+		asm volatile("s_nop 7\n\ts_nop 5\n\ts_waitcnt vmcnt(%0)" ::"n"(kMserTileStores) : "memory");
+		uint8_t* vb = vring + kMserVSlot * slot;
+		const uint8_t* rb = rring + 1024 * slot;
+		if (j + 1 < j1) {
+			N = F;
+			ser_job_next(a, N);
+			ser_job_dma(a, N, vring + kMserVSlot * (slot ^ 1u), rring + 1024 * (slot ^ 1u));
+			asm volatile("s_nop 7\n\ts_nop 6" ::: "memory");   // (the ISA check's marker: DMAs above)
+		}
+		// The next job's wait counts exactly one staged tile's stores after its
+		// DMAs; every other path through this job drains right where it
+		// departs from that (drain()), so the count holds on every path
+		// (tests/test_isa_serialize.py walks them).
+		auto drain = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+		const uint32_t vl = F.vl;
+		const uint8_t* V = a.ver + F.v_off;
+		const int64_t g0 = (int64_t)F.c * kMemChunk - 16;
+		if (F.st != 0) {
+			drain();
+		} else if (F.end > a.out_cap) {
+			if (F.c == 0 && lane == 0) a.status[F.pair] = 7;
+			drain();
+		} else {
+			uint8_t* out = a.out + F.base;
+			if (F.c == 0) {
+				put_header(out, vl);
+				drain();
+			}
+			if (!F.cnt) {
+				drain();
+			} else {
+				// the piece that straddles |V| (the pair's last chunk): from bytes
+				if (g0 + (int64_t)kStage > (int64_t)vl) {
+#pragma unroll
+					for (uint32_t k = 0; k < kStageRows; ++k) {
+						const int64_t p = g0 + 1024 * k + 16 * lane;
+						if (1024 * k + 16 * lane < kStage && p >= 0 && p < (int64_t)vl && p + 16 > (int64_t)vl) {
+							const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+							*(uint4*)(vb + 1024 * k + 16 * lane) = stage_piece(z, V, p, vl);
+						}
+					}
+					drain();
+				}
+				lds_order();
+				uint64_t pos = F.boff;
+				uint32_t prev_end = F.first;
+				// one tile of up to 64 members; tile 0 (records from the ring) is
+				// straight-line code, so every path through a job with members
+				// passes its fixed stores (or a drain)
+				auto tile = [&](uint32_t t0, const uint4& r) {
+					const bool valid = t0 + lane < F.cnt;
+					const uint32_t x = r.x, len = r.y;
+					const uint32_t last = valid ? x + len : 0u;
+					uint32_t prev = wave_shr1(last);
+					if (lane == 0) prev = prev_end;
+					const uint32_t gap = x - prev;
+					const uint32_t sz = valid ? 13u + (gap ? 9u + gap : 0u) : 0u;
+					const uint32_t incl = wave_incl_scan(sz);
+					const uint32_t my = incl - sz;
+					const uint32_t S = rdlane(incl, 63);
+					if (S <= kMserPipeStage) {
+						lds_order();
+						put_bulk(stage, valid, my, prev, x, len, r.z, vb, g0);
+						lds_order();
+						__builtin_amdgcn_s_waitcnt(0xc07f);
+						// flush as a fixed count of buffer stores: head bytes to a
+						// 16-byte boundary, 16-byte pieces, tail bytes (lanes past
+						// the end dropped by each descriptor's size)
+						uint8_t* dst = out + pos;
+						const uint32_t head = umin32((uint32_t)((16u - ((uintptr_t)dst & 15u)) & 15u), S);
+						const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)head, 0x00020000);
+						__builtin_amdgcn_raw_buffer_store_b8(stage[lane & 15u], rh, (int)lane, 0, 0);
+						const uint32_t nq = (S - head) / 16;
+						const __amdgpu_buffer_rsrc_t rq =
+						    __builtin_amdgcn_make_buffer_rsrc(dst + head, (short)0, (int)(16 * nq), 0x00020000);
+#pragma unroll
+						for (uint32_t i = 0; i < kMserPipeStage / 1024; ++i) {
+							const uint32_t k = lane + 64 * i;
+							const uint32_t o = umin32(head + 16 * k, kMserPipeStage);
+							uint32_t w[4];
+							__builtin_memcpy(w, stage + o, 16);
+							typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+							__builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, rq, (int)(16 * k), 0, 0);
+						}
+						const uint32_t tail0 = head + 16 * nq;
+						const __amdgpu_buffer_rsrc_t rt =
+						    __builtin_amdgcn_make_buffer_rsrc(dst + tail0, (short)0, (int)(S - tail0), 0x00020000);
+						__builtin_amdgcn_raw_buffer_store_b8(stage[umin32(tail0 + (lane & 15u), kMserPipeStage + 15)], rt, (int)lane, 0, 0);
+						__builtin_amdgcn_s_waitcnt(0xc07f);   // the stage's reads before its next writes
+					} else {
+						put_bulk(out + pos, valid, my, prev, x, len, r.z, vb, g0);
+						drain();
+					}
+					pos += S;
+					const uint64_t has = __ballot(valid);
+					prev_end = rdlane(last, 63u - (uint32_t)__builtin_clzll(has));
+				};
+				{
+					const lds32c* q = (const lds32c*)(rb + 16 * lane);
+					tile(0u, make_uint4(q[0], q[1], q[2], q[3]));
+				}
+				for (uint32_t t0 = 64; t0 < F.cnt; t0 += 64) {
+					drain();   // (the tile before flushed its stores)
+					uint4 r = make_uint4(0u, 0u, 0u, 0u);
+					if (t0 + lane < F.cnt) r = *(const uint4*)(a.srec + 4ull * (F.slot0 + t0 + lane));
+					tile(t0, r);
+					drain();
+				}
+			}
+			// the chain's own record runs and the tail (segments 2c, 2c + 1;
+			// the pair's last chunk takes the rest)
+			const uint32_t ns = ((c4_u32*)(a.nseg + F.pair))[0];
+			const uint32_t* seg = a.seg + 4ull * ((uint64_t)F.chunk_base + 2ull * F.pair);
+			const uint32_t k1 = F.c + 1 == F.n_chunks ? ns : umin32(2 * F.c + 2, ns);
+			for (uint32_t k = 2 * F.c; k < k1; ++k) {
+				const uint4 e = *(const uint4*)(seg + 4ull * k);
+				uint8_t* o = out + e.z;
+				if (e.x == kSegTail) {
+					const uint64_t n = put_tail(o, V, vl, e.w);
+					if (e.z + n != F.end - F.base && lane == 0) a.status[F.pair] = 12;   // DG_ERR_INTERNAL: sizes disagree
+				} else {
+					const RecWords src{a.rec + (uint64_t)kRecWordsOnepass * (F.rec_base + e.x), kRecWordsOnepass};
+					serialize_run<kMserPipeStage>(o, V, vl, src, e.y, e.w, (sw_lds8*)stage);
+				}
+				drain();
+			}
+		}
+		F = N;
+	}
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA outlives the wave
+}
+
 // staged_grid: the waves a dense batch uses; a sparse one (delta under half
 // of sum |V|) uses the whole grid (the launch gives it kSerWavesSparse per
 // CU): its jobs are bound by their dependent descriptor loads, and more,
 // shorter job ranges finish sooner (c6 1090 -> 1192 GiB/s), while a dense
 // batch's staging traffic is fastest at 16 waves per CU (C3 447 vs 435 at 24)
+#ifndef DG_MSER_PIPE   // A/B: 0 = round 5's member_serialize
+#define DG_MSER_PIPE 1
+#endif
 __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint32_t n_jobs, uint32_t staged_grid) {
+#if DG_MSER_PIPE
+	__shared__ __attribute__((aligned(16))) uint8_t vring[2 * kMserVSlot];
+	__shared__ __attribute__((aligned(16))) uint8_t rring[2 * 1024];
+	__shared__ __attribute__((aligned(16))) uint8_t stage[kMserPipeStage + 96];
+#else
 	__shared__ __attribute__((aligned(16))) uint8_t vbuf[kStage + 16];
 	__shared__ __attribute__((aligned(16))) uint8_t stage[kMemSerStage + 96];
+#endif
 	// (uniform for the launch: the scan's total is final before this kernel)
 	const uint64_t dtot = a.v_total ? uni64(a.offsets[a.n_pairs]) : ~0ull;
 	const uint32_t grid = dtot * 2 < a.v_total ? gridDim.x : umin32(gridDim.x, staged_grid);
@@ -1032,7 +1267,11 @@ __global__ __launch_bounds__(64) void member_serialize_kernel(MemSerArgs a, uint
 	const uint32_t j0 = a.job0 + (uint32_t)((uint64_t)n_jobs * blockIdx.x / grid);
 	const uint32_t j1 = a.job0 + (uint32_t)((uint64_t)n_jobs * (blockIdx.x + 1) / grid);
 	if (j0 >= j1) return;
+#if DG_MSER_PIPE
+	member_serialize_pipe(a, j0, j1, vring, rring, stage);
+#else
 	member_serialize(a, j0, j1, vbuf, stage);
+#endif
 }
 
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st) {

@@ -85,6 +85,14 @@ __device__ unsigned long long g_pair_prof[kPairProfMax * 4];
 #define PROF_ADD(o, i, v) ((void)0)
 #endif
 
+#ifdef DG_PAIR_TIME   // variant build: per pair start/end (s_memrealtime, 100 MHz) and placement
+constexpr uint32_t kPairTimeMax = 16384;
+__device__ unsigned long long g_pair_time[kPairTimeMax * 3];
+extern "C" int dg_pair_time_read(unsigned long long* out, int n) {
+	if (n > (int)kPairTimeMax) n = (int)kPairTimeMax;
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_time), 24ull * n) == hipSuccess ? n : -1;
+}
+#endif
 #ifdef DG_REFILL_PROF   // variant build: refill-wait cycles, refills, pair cycles
 __device__ unsigned long long g_refill_prof[3];
 extern "C" int dg_refill_prof_read(unsigned long long* out) {
@@ -1355,6 +1363,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #ifdef DG_REFILL_PROF
 	const uint64_t t_all0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef DG_PAIR_TIME
+	const uint64_t t_pt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 	const PairResult res = onepass_pair<kMembers, WinSrc, kRouted>(src, a, pair, pd, pp, 16u, bm, (uint32_t*)lcache);
 #ifdef DG_REFILL_PROF
 	if (lane_id() == 0) {
@@ -1364,6 +1375,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 	}
 #endif
 	vm_drain();   // no LDS-DMA may outlive the wave's LDS allocation
+#ifdef DG_PAIR_TIME
+	if (lane_id() == 0 && pair < kPairTimeMax) {
+		const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID: wave, simd, cu, se ...
+		const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // HW_REG_XCC_ID
+		g_pair_time[3ull * pair] = t_pt0;
+		g_pair_time[3ull * pair + 1] = __builtin_amdgcn_s_memrealtime();
+		g_pair_time[3ull * pair + 2] = ((unsigned long long)xcc << 32) | hw;
+	}
+#endif
 	if (!kMembers && !kRouted && a.lookback) {
 		// fused placement + serialisation (dg_serialize_wave.h)
 		const uint64_t off = lookback_offset(a.lookback, pair, res.dsz);

@@ -5,6 +5,8 @@
 // counter per class, and scripts/pmc_calib.py turns them into factors.
 //   stream16   coalesced 16 B/lane global loads          (CRC, staging)
 //   dma16      16 B/lane global_load_lds (LDS-DMA)       (onepass windows, member staging)
+//   stream8    coalesced 8 B/lane global loads           (CRC rows beside the onepass kernel)
+//   dma4       4 B/lane global_load_lds, coalesced       (the serialisers' record rings)
 //   rand16     one 16 B load per lane at a random 128 B line (onepass table tier)
 //   rand4      one 4 B load per lane at a random line    (correcting index probes)
 //   store16    coalesced 16 B/lane stores                 (serialisers, decode)
@@ -53,6 +55,28 @@ __global__ __launch_bounds__(64) void dma16(const uint8_t* p, size_t n, uint32_t
 	if (lds[lane] == 0xFF && lds[lane + 64] == 0xFE && lane == 77) sink[0] = 1;
 }
 
+__global__ __launch_bounds__(256) void stream8(const uint2* p, size_t n, uint32_t* sink) {
+	uint32_t acc = 0;
+	for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+		const uint2 v = p[i];
+		acc ^= v.x ^ v.y;
+	}
+	if (acc == 0x9u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(64) void dma4(const uint8_t* p, size_t n, uint32_t* sink) {
+	__shared__ __attribute__((aligned(16))) uint8_t lds[4096];
+	const uint32_t lane = threadIdx.x;
+	for (size_t o = (size_t)blockIdx.x * 4096; o < n; o += (size_t)gridDim.x * 4096) {
+#pragma unroll
+		for (int k = 0; k < 16; ++k)
+			__builtin_amdgcn_global_load_lds((const void*)(p + o + 256 * k + 4 * lane), (lds_void_t*)(lds + 256 * k), 4, 0, 0);
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	}
+	__syncthreads();
+	if (lds[lane] == 0xFF && lds[lane + 64] == 0xFE && lane == 77) sink[0] = 1;
+}
+
 // one load per lane: line perm(i), at a 16 B slot inside it chosen by i
 __global__ __launch_bounds__(256) void rand16(const uint8_t* p, uint32_t n, uint32_t* sink) {
 	const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -95,6 +119,8 @@ int main(int argc, char** argv) {
 	// known bytes per launch (printed for pmc_calib.py)
 	if (on("stream16")) { hipLaunchKernelGGL(stream16, dim3(2048), dim3(256), 0, 0, (const uint4*)a, kBytes / 16, sink); printf("stream16 %zu\n", kBytes); }
 	if (on("dma16")) { hipLaunchKernelGGL(dma16, dim3(8192), dim3(64), 0, 0, a, kBytes, sink); printf("dma16 %zu\n", kBytes); }
+	if (on("stream8")) { hipLaunchKernelGGL(stream8, dim3(2048), dim3(256), 0, 0, (const uint2*)a, kBytes / 8, sink); printf("stream8 %zu\n", kBytes); }
+	if (on("dma4")) { hipLaunchKernelGGL(dma4, dim3(8192), dim3(64), 0, 0, a, kBytes, sink); printf("dma4 %zu\n", kBytes); }
 	if (on("rand16")) { hipLaunchKernelGGL(rand16, dim3(nr / 256), dim3(256), 0, 0, a, nr, sink); printf("rand16 %zu\n", (size_t)nr * 16); }
 	if (on("rand4")) { hipLaunchKernelGGL(rand4, dim3(nr / 256), dim3(256), 0, 0, a, nr, sink); printf("rand4 %zu\n", (size_t)nr * 4); }
 	if (on("store16")) { hipLaunchKernelGGL(store16, dim3(2048), dim3(256), 0, 0, (uint4*)b, kBytes / 16); printf("store16 %zu\n", kBytes); }

@@ -22,7 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KNOWN = {   # pmc_calib.cpp: bytes each kernel moves per launch (2 GiB buffers, 16 Mi lines)
-    "stream16": 2 << 30, "dma16": 2 << 30, "rand16": (16 << 20) * 16, "rand4": (16 << 20) * 4,
+    "stream16": 2 << 30, "dma16": 2 << 30, "stream8": 2 << 30, "dma4": 2 << 30, "rand16": (16 << 20) * 16, "rand4": (16 << 20) * 4,
     "store16": 2 << 30, "store16r": (16 << 20) * 16,
 }
 # the dominant kernel(s) of each line, as bench.py names them, and the
@@ -39,6 +39,15 @@ DOMINANT = {
 # FETCH class of each dominant kernel's reads (pmc_calib factors apply per class)
 FETCH_CLASS = {"onepass16_kernel": "dma16", "member_chunk_kernel": "dma16", "decode_kernel": "stream16",
                "correcting_build_kernel + correcting_scan_kernel": "stream16"}
+
+
+# the access class of each kernel of a step (path-level traffic): the first
+# pattern that matches names the pmc_calib class whose factor applies
+PATH_CLASS = [(r"onepass16_kernel|member_chunk_kernel|onepass_kernel", "dma16"),
+              (r"crc_rows_wide", "stream16"), (r"crc_rows_kernel", "stream8"),
+              (r"correcting_build", "stream16"), (r"decode_kernel", "stream16"),
+              (r"serialize_wave_kernel|member_serialize_kernel", "dma4")]
+CALIB_DEFAULT = {"dma16": 2.0, "stream16": 2.0}
 
 
 def stats_rows(path):
@@ -168,6 +177,41 @@ def main():
                                  "hbm_bytes_upper: x 2 (every request 128 B tallied at 64 B, as streaming reads); "
                                  "WRITE_SIZE KiB x 1024")
         json.dump(res, open(os.path.join(prof, f"{tag}_pmc_traffic_{cfg}.json"), "w"), indent=1)
+    # ── path-level traffic: every kernel of a step (scripts/profile_round.sh path) ──
+    for d in sorted(glob.glob(os.path.join(src, "path_*_FETCH_SIZE"))):
+        if not os.path.isdir(d):
+            continue
+        cfg = os.path.basename(d)[5:-len("_FETCH_SIZE")]
+        f, nf = counter(d, "FETCH_SIZE")
+        w, nw = counter(os.path.join(src, f"path_{cfg}_WRITE_SIZE"), "WRITE_SIZE")
+        bj = os.path.join(src, f"path_{cfg}_FETCH_SIZE.json")
+        bline = json.load(open(bj)) if os.path.exists(bj) else {}
+        path_bytes = (bline.get("roofline") or {}).get("path_bytes_per_step")
+        kern, lo, hi = {}, 0.0, 0.0
+        for k in sorted(set(f) | set(w)):
+            cls = next((c for p, c in PATH_CLASS if re.search(p, k)), None)
+            fac = (calib.get(cls) or {}).get("bytes_per_fetch_kib") or CALIB_DEFAULT.get(cls, 1.0) if cls else 1.0
+            fk = (f.get(k) or 0.0) * 1024
+            wk = (w.get(k) or 0.0) * 1024
+            k_lo = fk * fac + wk
+            k_hi = fk * max(fac, 2.0) + wk
+            lo += k_lo
+            hi += k_hi
+            kern[k] = {"fetch_kib": f.get(k), "write_kib": w.get(k), "dispatches": [nf.get(k), nw.get(k)],
+                       "fetch_class": cls or "small / random (x1 lower, x2 upper)", "fetch_factor": round(fac, 4),
+                       "hbm_bytes": int(k_lo), "hbm_bytes_upper": int(k_hi)}
+        res = {"config": cfg, "lib_sha16": bline.get("lib_sha16"), "kernels": kern,
+               "path_traffic_per_step": int(lo), "path_traffic_upper_per_step": int(hi),
+               "path_bytes_per_step": path_bytes,
+               "ratio": round(lo / path_bytes, 3) if path_bytes else None,
+               "ratio_upper": round(hi / path_bytes, 3) if path_bytes else None,
+               "correction": "per kernel: FETCH_SIZE KiB x 1024 x its access class's factor "
+                             f"(profiles/{tag}_pmc_calib.json; classes without one x1), + WRITE_SIZE KiB x 1024; "
+                             "upper: every FETCH at least x2",
+               "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-include-regex dg:: --kernel-exclude-regex "
+                          f"synth -- python3 bench.py --config {cfg} --also none --steps 5 --warmup 1"}
+        json.dump(res, open(os.path.join(prof, f"{tag}_pmc_path_{cfg}.json"), "w"), indent=1)
+        print("path", cfg, res["path_traffic_per_step"], res["ratio"], res["ratio_upper"])
     # ── fresh-plan warm-up: per-dispatch durations of each config's dominant
     #    kernel in launch order (the checked step, the profile pass, warmup, timed) ──
     warm = {}

@@ -4,7 +4,9 @@
 #         (bench.py --config C --also none), its bench line beside it
 #   calib FETCH_SIZE / WRITE_SIZE of scripts/micro/pmc_calib per access class
 #   pmc   FETCH_SIZE / WRITE_SIZE passes of each config's dominant kernel(s)
-# usage: scripts/profile_round.sh TAG [ks|calib|pmc|all] [CONFIGS...]
+#   path  FETCH_SIZE / WRITE_SIZE passes of every kernel of a step (all dg::
+#         kernels but the input synthesis), for the path-level traffic
+# usage: scripts/profile_round.sh TAG [ks|calib|pmc|path|all] [CONFIGS...]
 # Outputs under gpurun_out/TAG/; scripts/profile_collect.py TAG copies the
 # summaries into profiles/.
 set -o pipefail
@@ -24,7 +26,7 @@ if [ "$WHAT" = ks ] || [ "$WHAT" = all ]; then
   done
 fi
 if [ "$WHAT" = calib ] || [ "$WHAT" = all ]; then
-  for k in stream16 dma16 rand16 rand4 store16 store16r; do
+  for k in ${CALIB:-stream16 dma16 stream8 dma4 rand16 rand4 store16 store16r}; do
     for c in FETCH_SIZE WRITE_SIZE; do
       timeout -s KILL 60 rocprofv3 --pmc $c --kernel-include-regex "^$k" --output-format csv -d $O/calib_${k}_$c -o pmc -- \
           scripts/micro/pmc_calib $k > $O/calib_${k}_$c.log 2>&1 || { echo "calib $k $c rc=$?"; tail -5 $O/calib_${k}_$c.log; exit 1; }
@@ -48,6 +50,18 @@ if [ "$WHAT" = pmc ] || [ "$WHAT" = all ]; then
           --full-out $O/pmc_${c}_$p.json > $O/pmc_${c}_$p.log 2>&1 || { echo "pmc $c $p rc=$?"; tail -5 $O/pmc_${c}_$p.log; exit 1; }
     done
     echo "pmc $c done"
+  done
+fi
+if [ "$WHAT" = path ] || [ "$WHAT" = all ]; then
+  for c in $CFGS; do
+    case $c in c2|c3|c4|c6|c2_defq) ;; *) continue ;; esac
+    for p in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 300 rocprofv3 --pmc $p --kernel-include-regex "dg::" --kernel-exclude-regex "synth" \
+          --output-format csv -d $O/path_${c}_$p -o pmc -- \
+          python3 bench.py --config $c --also none --steps 5 --warmup 1 --no-cpu-baseline --no-e2e \
+          --full-out $O/path_${c}_$p.json > $O/path_${c}_$p.log 2>&1 || { echo "path $c $p rc=$?"; tail -5 $O/path_${c}_$p.log; exit 1; }
+    done
+    echo "path $c done"
   done
 fi
 echo profile_round done

@@ -1,18 +1,19 @@
 """ISA check of the serialisers' hand-counted wait.
 
-`serialize_run` (csrc/dg_serialize_wave.h) loads the next tile's COPY records
-with inline-asm `global_load_dword`s the compiler does not see, then trusts
-`s_waitcnt vmcnt(N)` at the end of the tile.  VMEM operations complete in issue
-order, so that wait covers the loads only if at least N VMEM operations were
-issued after them on every path (or an earlier wait already covered them), and
-nothing may read or write the loads' registers before that.  A compiler change
-that merges, splits or adds a VMEM operation there, or copies a destination
-register early, would make the records silently wrong.
+`serialize_run` (csrc/dg_serialize_wave.h) loads the next tile's records into
+registers by inline asm, and the member serialiser's pipeline (and the A/B
+`serialize_pipe`) load what a later tile needs by LDS-DMA into rings; each
+trusts one `s_waitcnt vmcnt(N)` before the loaded words are used.  VMEM operations complete in
+issue order, so that wait covers the DMAs only if at least N VMEM operations
+were issued after them on every path (or an earlier wait already covered
+them).  A compiler change that merges, splits or adds a VMEM operation there
+would make the records silently wrong; and nothing may read or write a
+register load's destination before the wait covers it.
 
 This test disassembles the built gfx950 code object (CPU only, no GPU), finds
-the asm markers (`s_nop 5` after the four loads, `s_nop 4` before each wait),
-builds the control-flow graph of `serialize_wave_kernel` and
-`member_serialize_kernel`, and walks every path from each load group.
+the asm markers (`s_nop 7; s_nop 6` after the DMAs, `s_nop 7; s_nop 4` after
+register loads, `s_nop 7; s_nop 5` before each counted wait), builds the control-flow graph of `serialize_wave_kernel`
+and `member_serialize_kernel` and walks every path from each DMA group.
 """
 from __future__ import annotations
 
@@ -102,21 +103,30 @@ def _check_kernel(ins, base, raw_lines):
             return fall + [addr_ix[target[a]]]
         return fall
 
-    groups = []   # (index after the marker, destination registers)
-    for i in range(4, len(ins)):
-        if ins[i][1] == "s_nop" and ins[i][2].startswith("5") and all(
-                ins[i - k][1] == "global_load_dword" for k in range(1, 5)):
+    groups = []   # (index after the marker, destination registers: none for LDS-DMA)
+    for i in range(1, len(ins) - 1):
+        if not (ins[i][1] == "s_nop" and ins[i][2].startswith("7") and ins[i + 1][1] == "s_nop"):
+            continue
+        if ins[i + 1][2].startswith("6"):     # LDS-DMA group (serialize_pipe, member pipeline)
+            assert any(ins[i - k][1].startswith("global_load_lds") for k in range(1, 6) if i - k >= 0), \
+                f"{ins[i][0]:#x}: DMA marker without a DMA before it"
+            groups.append((i + 2, set()))
+        elif ins[i + 1][2].startswith("4"):   # register loads (serialize_run's rec_load4)
+            loads = ins[i - 4:i]
+            assert all(mn == "global_load_dword" for _, mn, _ in loads), \
+                f"{ins[i][0]:#x}: load marker without the four record loads before it"
             dst = set()
-            for k in range(1, 5):
-                dst |= _regs(ins[i - k][2].split(",")[0])
-            groups.append((i + 1, dst))
-    waits = {i + 1 for i in range(len(ins) - 1)
-             if ins[i][1] == "s_nop" and ins[i][2].startswith("4") and ins[i + 1][1] == "s_waitcnt"}
-    assert groups, "record-load marker not found"
+            for _, _, ops in loads:
+                dst |= _regs(ops.split(",")[0])
+            groups.append((i + 2, dst))
+    waits = {i + 2 for i in range(len(ins) - 2)
+             if ins[i][1] == "s_nop" and ins[i][2].startswith("7") and ins[i + 1][1] == "s_nop"
+             and ins[i + 1][2].startswith("5") and ins[i + 2][1] == "s_waitcnt"}
+    assert groups, "DMA marker not found"
     assert waits, "wait marker not found"
     checked = 0
     for start, dst in groups:
-        assert len(dst) == 4, dst
+        assert len(dst) in (0, 4), dst
         # states: (instruction index, VMEM ops issued since the loads (capped),
         # known wave-uniform flags).  The compiler joins if/else arms through
         # a flag SGPR pair (s_mov_b64 s[a:b], -1 / 0 ... s_and_b64 vcc, exec,
@@ -143,9 +153,20 @@ def _check_kernel(ins, base, raw_lines):
                                      f"before the wait covers their loads")
             if VMEM.match(mn):
                 n = min(n + 1, 64)
-            nexts = succ(i)
             first = ops.split(",")[0].strip() if ops else ""
-            if mn in ("s_cbranch_vccz", "s_cbranch_vccnz") and "vcc" in kd:
+            nexts = succ(i)
+            # exec: full in the uniform code the walk starts in; a wave whose
+            # exec may be empty is one inside a divergent region
+            if first == "exec" and not mn.startswith("s_cbranch"):
+                if mn.startswith("s_or_b64") and "exec, exec" in ops:
+                    kd.pop("exec_low", None)              # the region's mask restored
+                elif not (mn == "s_mov_b64" and ops.split(",")[1].strip() == "-1"):
+                    kd["exec_low"] = 1
+            elif mn.endswith("saveexec_b64"):
+                kd["exec_low"] = 1
+            if mn in ("s_cbranch_execz", "s_cbranch_execnz") and "exec_low" not in kd:
+                nexts = [nexts[0]] if mn == "s_cbranch_execz" else [nexts[1]]
+            elif mn in ("s_cbranch_vccz", "s_cbranch_vccnz") and "vcc" in kd:
                 taken = (kd["vcc"] == 0) == (mn == "s_cbranch_vccz")
                 nexts = [nexts[1]] if taken else [nexts[0]]
             elif mn == "s_mov_b64" and re.fullmatch(r"s\[\d+:\d+\]", first) and ops.split(",")[1].strip() in ("0", "-1"):
@@ -200,13 +221,13 @@ def test_serialiser_record_wait_is_counted(kernel):
                 raw.append((int(m.group(3), 16), line))
             elif not line.strip() and raw:
                 break
-    assert _check_kernel(ins, base, raw) >= 2   # the first tile's loads and the next tile's
+    assert _check_kernel(ins, base, raw) >= 1
 
 
 @pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists(OBJDUMP), reason="library or llvm-objdump missing")
-def test_checker_rejects_a_short_count_and_an_early_read():
+def test_checker_rejects_a_short_count_and_a_missing_store():
     """The checker itself: the same instructions with the counted wait raised
-    by one, or with a copy of a record register placed before the wait, fail."""
+    by one, or with one of the tile's stores gone, fail."""
     kernel = "serialize_wave_kernel"
     with tempfile.TemporaryDirectory() as tmp:
         dis = _gfx950_disasm(tmp)
@@ -223,20 +244,21 @@ def test_checker_rejects_a_short_count_and_an_early_read():
                 raw.append((int(m.group(3), 16), line))
             elif not line.strip() and raw:
                 break
-    assert _check_kernel(ins, base, raw) >= 2
-    # (a) the counted wait one higher than the stores behind the loads
-    w = next(i + 1 for i in range(len(ins) - 1) if ins[i][1] == "s_nop" and ins[i][2].startswith("4")
-             and re.search(r"vmcnt\(([1-9]\d*)\)", ins[i + 1][2]))
+    assert _check_kernel(ins, base, raw) >= 1
+    # (a) the counted wait one higher than the stores behind the DMAs
+    w = next(i + 2 for i in range(len(ins) - 2) if ins[i][1] == "s_nop" and ins[i][2].startswith("7")
+             and ins[i + 1][1] == "s_nop" and ins[i + 1][2].startswith("5")
+             and re.search(r"vmcnt\(([1-9]\d*)\)", ins[i + 2][2]))
     k = int(re.search(r"vmcnt\((\d+)\)", ins[w][2]).group(1))
     bad = list(ins)
     bad[w] = (ins[w][0], "s_waitcnt", f"vmcnt({k + 1})")
     with pytest.raises(AssertionError, match="may not have landed"):
         _check_kernel(bad, base, raw)
-    # (b) a copy of a record register right after a load group
-    g = [i for i in range(4, len(ins)) if ins[i][1] == "s_nop" and ins[i][2].startswith("5")][-1]   # in the loop
-    reg = ins[g - 1][2].split(",")[0].strip()
-    j = next(i for i in range(g + 1, len(ins)) if not ins[i][1].startswith(("s_", "global_", "buffer_")))
+    # (b) one buffer store of the staged flush (the last one before the wait) gone
+    j = max(i for i in range(w) if ins[i][1].startswith("buffer_store"))
     bad = list(ins)
-    bad[j] = (ins[j][0], "v_mov_b32", f"v0, {reg}")
-    with pytest.raises(AssertionError, match="touches the record registers"):
+    bad[j] = (ins[j][0], "s_nop", "0")
+    with pytest.raises(AssertionError, match="may not have landed"):
         _check_kernel(bad, base, raw)
+
+
