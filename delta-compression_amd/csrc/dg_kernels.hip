@@ -105,8 +105,12 @@ __global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a)
 #ifndef DG_CRC_PF
 #define DG_CRC_PF 2
 #endif
+#ifndef DG_CRC_PRIO   // A/B: issue priority of the rows pass beside another kernel (0..3)
+#define DG_CRC_PRIO 0
+#endif
 template <int TAB>
 __global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
+	if constexpr (DG_CRC_PRIO > 0) __builtin_amdgcn_s_setprio(DG_CRC_PRIO);
 	constexpr uint32_t nt = TAB == kCrcByte ? 8 * 256 : 32 * kCrc5Tabs8;
 	__shared__ __attribute__((aligned(256))) uint64_t T8[nt];
 	for (uint32_t i = threadIdx.x; i < nt; i += 256) T8[i] = a.tables[(TAB == kCrcByte ? kCrcRows8 : kCrc5R8) + i];
@@ -615,6 +619,43 @@ __device__ __forceinline__ DecCmd dec_cmd(WP w, const uint16_t* cmds, uint32_t b
 typedef uint32_t u32x4_u __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t u32_u __attribute__((aligned(1)));
 
+// A command's last, partial 16-byte chunk (1 <= rem < 16 bytes).  Every load
+// is issued before any store, so the chunk costs one memory round trip: the
+// dwords at offsets 0, 4, 8, 12 clamped to rem - 4 (the last one overlaps the
+// one before it and stores the same bytes again), or, under 4 bytes, the
+// bytes at offsets clamped to rem - 1; never a byte outside [0, rem).
+// (Round 5 copied dword by dword and byte by byte, each store before the next
+// load: up to 6 dependent round trips per partial chunk.)
+#ifndef DG_DEC_TAIL1   // A/B: 0 = round 5's dword-then-byte loop
+#define DG_DEC_TAIL1 1
+#endif
+__device__ __forceinline__ void copy_tail(uint8_t* d, const uint8_t* s, uint32_t rem) {
+#if DG_DEC_TAIL1
+	if (rem >= 4) {
+		uint32_t w[4], o[4];
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			o[k] = umin32(4 * k, rem - 4);
+			w[k] = *reinterpret_cast<const u32_u*>(s + o[k]);
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k)
+			if (4 * k < rem) *reinterpret_cast<u32_u*>(d + o[k]) = w[k];
+	} else {
+		uint8_t b[3];
+#pragma unroll
+		for (uint32_t k = 0; k < 3; ++k) b[k] = s[umin32(k, rem - 1)];
+#pragma unroll
+		for (uint32_t k = 0; k < 3; ++k)
+			if (k < rem) d[k] = b[k];
+	}
+#else
+	const uint32_t nd = rem >> 2;
+	for (uint32_t k = 0; k < nd; ++k) *reinterpret_cast<u32_u*>(d + 4 * k) = *reinterpret_cast<const u32_u*>(s + 4 * k);
+	for (uint32_t k = 4 * nd; k < rem; ++k) d[k] = s[k];
+#endif
+}
+
 // Per-wave LDS scratch of the flat copy.
 struct DecScratch {
 	uint32_t* cum;        // [64] chunk prefix per non-empty command
@@ -693,10 +734,7 @@ __device__ void dec_flat_batch(const DecCmd& c, bool inplace, uint8_t* O, const 
 				if (rem[uu] >= 16) {
 					*reinterpret_cast<u32x4_u*>(da[uu]) = v[uu];
 				} else if (rem[uu]) {   // the command's last, partial chunk
-					const uint32_t nd = rem[uu] >> 2;
-					for (uint32_t k = 0; k < nd; ++k)
-						*reinterpret_cast<u32_u*>(da[uu] + 4 * k) = *reinterpret_cast<const u32_u*>(sa[uu] + 4 * k);
-					for (uint32_t k = 4 * nd; k < rem[uu]; ++k) da[uu][k] = sa[uu][k];
+					copy_tail(da[uu], sa[uu], rem[uu]);
 				}
 			}
 		}
@@ -928,10 +966,7 @@ __device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uin
 					if (rem[u] >= 16) {
 						*reinterpret_cast<u32x4_u*>(da[u]) = v[u];
 					} else if (rem[u]) {   // the command's last, partial chunk
-						const uint32_t nd = rem[u] >> 2;
-						for (uint32_t i = 0; i < nd; ++i)
-							*reinterpret_cast<u32_u*>(da[u] + 4 * i) = *reinterpret_cast<const u32_u*>(sa[u] + 4 * i);
-						for (uint32_t i = 4 * nd; i < rem[u]; ++i) da[u][i] = sa[u][i];
+						copy_tail(da[u], sa[u], rem[u]);
 					}
 				}
 			}
@@ -944,6 +979,11 @@ __device__ void dec_grouped_window(WP w, const uint16_t* cmds, uint32_t cnt, uin
 // (dg_crc.h).  The byte tables go to LDS at tb (256-byte aligned, inside the
 // dead doubling arrays), then the nibble table of x^(8 * 64 KiB) (the Horner
 // step of a wave's segments) at TK.
+#ifndef DG_DEC_CRC5   // A/B: the decode's CRC folds by five-bit tables (13 conflict-free lookups per piece)
+#define DG_DEC_CRC5 0
+#endif
+constexpr int kDecTab = DG_DEC_CRC5 ? kCrcFive : kCrcByte;
+constexpr uint32_t kDecTabWords = kDecTab == kCrcFive ? 32 * kCrc5Tabs8 : 8 * 256;
 struct DecCrc {
 	uint32_t tb;
 	const uint64_t* TK;
@@ -953,8 +993,9 @@ __device__ __forceinline__ DecCrc dec_crc_tables(uint16_t* NX, const DecodeArgs&
 	const uint32_t tid = threadIdx.x;
 	const uint32_t base = lds_addr(NX), tb = (base + 255u) & ~255u;
 	uint64_t* T = reinterpret_cast<uint64_t*>(NX) + (tb - base) / 8;
-	for (uint32_t k = tid; k < 8 * 256; k += kDecBlock) T[k] = a.tables[kCrcRows8 + k];
-	uint64_t* TK = T + 8 * 256;
+	const uint64_t* src = a.tables + (kDecTab == kCrcFive ? kCrc5R8 : kCrcRows8);
+	for (uint32_t k = tid; k < kDecTabWords; k += kDecBlock) T[k] = src[k];
+	uint64_t* TK = T + kDecTabWords;
 	const uint64_t* KF = a.tables + 8 * 256 + kCrcLevels * kCrcNibTabWords;
 	for (uint32_t k = tid; k < kCrcNibTabWords; k += kDecBlock) TK[k] = KF[k];   // x^(8 * 64 KiB)
 	static_assert(8 * (8 * 256 + kCrcNibTabWords) + 256 <= 3 * kDecWin * 2, "CRC tables fit NX");
@@ -963,7 +1004,7 @@ __device__ __forceinline__ DecCrc dec_crc_tables(uint16_t* NX, const DecodeArgs&
 template <bool kCopy = false>
 __device__ __forceinline__ uint64_t dec_seg_crc(const DecCrc& t, uintptr_t start, uint64_t len, uint32_t nseg,
                                                 uint32_t j, intptr_t copy_delta = 0, uintptr_t copy_hi = 0) {
-	return crc_seg_rows<8, 1, 8, kDecCrcSeg, kCopy>(start, len, nseg, j, t.tb, t.tb, t.klane, copy_delta, copy_hi);
+	return crc_seg_rows<8, 1, 8, kDecCrcSeg, kCopy, kDecTab>(start, len, nseg, j, t.tb, t.tb, t.klane, copy_delta, copy_hi);
 }
 
 __global__ __launch_bounds__(kDecBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void decode_kernel(DecodeArgs a) {

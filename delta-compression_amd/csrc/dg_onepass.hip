@@ -227,6 +227,10 @@ constexpr uint32_t kBackoffMax = DG_BACKOFF_MAX;   // tier backoff: at most 2^k 
 #ifndef DG_REFILL_TOUCH
 #define DG_REFILL_TOUCH 0
 #endif
+#ifndef DG_PRIO_PROGRESS   // issue priority by progress through V (set at each V refill); 0: A/B
+#define DG_PRIO_PROGRESS 1
+#endif
+constexpr bool kPrioProgress = DG_PRIO_PROGRESS != 0;
 constexpr uint32_t kTouchAhead = DG_REFILL_TOUCH;   // bytes past a refilled window warmed in the caches
 static_assert(kTouchAhead % 128 == 0 && kTouchAhead <= 8192, "one lane per 128-byte line");
 constexpr bool kDiagWinLim = DG_DIAG_WINLIM != 0;    // diagonal batch scans what the windows hold first
@@ -312,6 +316,19 @@ struct WinSrc {
 					const uint32_t off = base[1] + kWin + 128 * lane;
 					if (off < len[1]) __builtin_amdgcn_global_load_lds((const void*)(S[1] + off), (lds_void_t*)touch, 4, 0, 0);
 				}
+			}
+		}
+		if constexpr (kPrioProgress) {
+			// issue priority by progress through V: a wave behind the others
+			// on its SIMD outranks them, so the SIMD's waves finish together
+			// instead of oldest first (C2 per-pair durations p10..max 166..244
+			// -> 185..232 us, c3s_chain +4 %: profiles/r06_experiments.md)
+			if (fv) {
+				const uint64_t b4 = 4ull * base[0], l = len[0];
+				if (b4 < l) __builtin_amdgcn_s_setprio(3);
+				else if (b4 < 2 * l) __builtin_amdgcn_s_setprio(2);
+				else if (b4 < 3 * l) __builtin_amdgcn_s_setprio(1);
+				else __builtin_amdgcn_s_setprio(0);
 			}
 		}
 		PROF_ADD(*this, P_REFILLS, 1);

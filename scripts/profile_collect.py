@@ -178,6 +178,10 @@ def main():
                                  "WRITE_SIZE KiB x 1024")
         json.dump(res, open(os.path.join(prof, f"{tag}_pmc_traffic_{cfg}.json"), "w"), indent=1)
     # ── path-level traffic: every kernel of a step (scripts/profile_round.sh path) ──
+    if not calib:   # this session ran no calibration: the newest committed one
+        cf = sorted(glob.glob(os.path.join(prof, "r*_pmc_calib.json")))
+        if cf:
+            calib = json.load(open(cf[-1]))["classes"]
     for d in sorted(glob.glob(os.path.join(src, "path_*_FETCH_SIZE"))):
         if not os.path.isdir(d):
             continue
