@@ -426,6 +426,7 @@ struct dg_encode_plan {
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
 	uint32_t corr_lds_cap = 0; // correcting: R indexes up to this many slots built in LDS (DG_CORR_BUILD=global: none)
 	bool crc_fused = false;    // correcting: R's CRC computed by the LDS build, V's forked after it
+	bool op_crc = false;       // onepass plain plans: both CRCs computed by the onepass waves (no CRC pass)
 	bool crc_wide = false;     // correcting: R's and V's CRC in one wide-table pass before the build
 	bool crc_wide_beside = false;   // ... or forked after the build, beside the V scan
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
@@ -564,6 +565,27 @@ void dg::print_verbose(const dg_encode_plan_t* P, uint32_t i, const uint64_t* st
 }
 
 extern "C" {
+
+// member mode wanted for this batch (automatic choice by mean pair size:
+// measured C3 (256 KiB pairs) +56 %, C2 (64 KiB pairs) -22 %,
+// profiles/r02_experiments.md); the context's mode and the A/B switches
+// DG_NO_MEMBERS / DG_MEMBERS override it
+static bool members_wanted(const dg_context_t* ctx, const dg_pair_t* pairs, uint32_t n) {
+	uint64_t vsum = 0;
+	for (uint32_t i = 0; i < n; ++i) vsum += pairs[i].v_len;
+	bool want = n && vsum / n >= (128u << 10);
+	if (ctx->onepass_members == 1) want = true;
+	if (ctx->onepass_members == 2) want = false;
+	const char* nm = ab_env("DG_NO_MEMBERS");
+	if (nm && nm[0] == '1') want = false;
+	const char* fm = ab_env("DG_MEMBERS");
+	if (fm && fm[0] == '1') want = true;
+	return want;
+}
+#ifndef DG_OP_CRC_DEFAULT   // 1 (A/B): onepass plain plans compute their CRCs in the onepass waves
+#define DG_OP_CRC_DEFAULT 0   // (measured slower: C2 1786 -> 1172 GiB/s, profiles/r06_experiments.md)
+#endif
+constexpr bool kOpCrcDefault = DG_OP_CRC_DEFAULT != 0;
 
 int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_t* pairs,
                           uint32_t n, const dg_diff_options_t* opts, dg_encode_plan_t** out) {
@@ -718,11 +740,25 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			P->pp[i].crc_unpad = it->second;
 		}
 	}
-	// CRC spans: 2 per pair (R then V; V only when the build computes R's);
-	// arena offsets are rebased at run time
+	// onepass plain plans (the LDS-window chain, no member mode, no in-kernel
+	// serialisation) with DG_OP_CRC_DEFAULT=1: the onepass waves compute both
+	// CRCs from the bytes their windows stage (onepass16_crc_kernel), so no
+	// CRC pass reads R and V a second time.  Off in the product: the folds
+	// lengthen every wave's latency-bound chain (C2 kernel 0.221 -> 0.375 ms)
+	// by far more than the rows pass beside it costs the step (~0.02 ms).
+	// DG_OP_CRC=0 (A/B builds) turns it off in such a build.
+	{
+		const char* oc = ab_env("DG_OP_CRC");
+		const char* fz = ab_env("DG_FUSED");
+		P->op_crc = kOpCrcDefault && algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
+		            !(fz && fz[0] == '1') && !members_wanted(ctx, pairs, n) && !(oc && oc[0] == '0');
+	}
+	// CRC spans: 2 per pair (R then V; V only when the build computes R's;
+	// none when the onepass waves compute both); arena offsets are rebased at
+	// run time
 	std::vector<dg_span_t> spans;
 	std::vector<uint32_t> which, outs;
-	for (uint32_t i = 0; i < n; ++i) {
+	for (uint32_t i = 0; i < n && !P->op_crc; ++i) {
 		if (!P->crc_fused || P->pp[i].q > P->corr_lds_cap) {
 			spans.push_back(dg_span_t{pairs[i].r_off, pairs[i].r_len});
 			which.push_back(0);
@@ -796,15 +832,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		// (profiles/r02_experiments.md) C3 (256 KiB pairs) +56 %, C2 (64 KiB
 		// pairs, where the plain chain's latency-bound waves overlap the CRC)
 		// -22 %
-		uint64_t vsum = 0;
-		for (uint32_t i = 0; i < n; ++i) vsum += pairs[i].v_len;
-		bool want = n && vsum / n >= (128u << 10);
-		if (ctx->onepass_members == 1) want = true;
-		if (ctx->onepass_members == 2) want = false;
-		const char* nm = ab_env("DG_NO_MEMBERS");
-		if (nm && nm[0] == '1') want = false;
-		const char* fm = ab_env("DG_MEMBERS");
-		if (fm && fm[0] == '1') want = true;
+		const bool want = members_wanted(ctx, pairs, n);
 		P->members = algo == DG_ALGO_ONEPASS && o.p == 16 && P->aligned16 && onepass16_selected() &&
 		             !P->fused && want;
 		// automatic mode: a pair averaging fewer than 2 verified members per
@@ -1178,6 +1206,10 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				HIPCHK(ctx, rec(6, st));
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			} else {
+				if (P->op_crc) {
+					a.crc_out = P->d_crc.as<uint64_t>();
+					a.crc_tab = ctx->d_crc_tables;
+				}
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			}
 		} else {

@@ -45,6 +45,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "dg_crc.h"
 #include "dg_device.h"
 #include "dg_devutil.h"
 #include "dg_serialize_wave.h"
@@ -236,8 +237,11 @@ static_assert(kTouchAhead % 128 == 0 && kTouchAhead <= 8192, "one lane per 128-b
 constexpr bool kDiagWinLim = DG_DIAG_WINLIM != 0;    // diagonal batch scans what the windows hold first
 constexpr uint32_t kDiagMinScan = DG_DIAG_MINSCAN;  // ... when that is at least this many bytes
 
-// p = 16 and 16-byte aligned stream bases: sliding LDS windows.
-struct WinSrc {
+// p = 16 and 16-byte aligned stream bases: sliding LDS windows.  kCrc: the
+// wave also computes both streams' CRC-64/XZ (onepass16_crc_kernel), folding
+// the rows its windows hold (crc_fold_window, between epochs).
+template <bool kCrc = false>
+struct WinSrcT {
 	static constexpr bool kPhaseA = true;
 	static constexpr uint32_t kBmWords = 128;  // phase-B bitmap: 4096 bits per table (bm[256])
 	const uint8_t* S[2];     // V, R (16-byte aligned)
@@ -251,6 +255,15 @@ struct WinSrc {
 	// (Keeping it across calls measured +2.5 % at C3, -6 % at C2: removed.)
 	uint16_t* lc;            // kListCap entries
 	uint32_t lc_base = 0, lc_n = 0;
+	// kCrc: per stream (0 = V, 1 = R) the CRC row fold of dg_crc.h over one
+	// segment of crow_n rows of 64 x 8 bytes tiled back from the stream's
+	// 16-byte aligned end (row 0 starts cdom <= 0 bytes from the stream's
+	// first byte; bytes outside the stream read as zeros), lane l folding
+	// piece l of every row into (cy_lo, cy_hi); crow = the next row to fold
+	uint32_t crc_tb = 0;     // LDS byte address of the five-bit row tables
+	uint32_t cy_lo[2] = {0u, 0u}, cy_hi[2] = {0u, 0u};
+	uint32_t crow[2] = {0u, 0u}, crow_n[2] = {0u, 0u};
+	int32_t cdom[2] = {0, 0};
 	PROF_DECL
 #ifdef DG_REFILL_PROF
 	uint64_t refill_cycles = 0;
@@ -265,7 +278,12 @@ struct WinSrc {
 		if (!fv && !fr) return;
 		[[maybe_unused]] const uint64_t t0 = PROF_NOW_R();
 		const uint32_t lane = lane_id();
-		__syncthreads();   // the wave's reads of the old window are complete
+		if constexpr (kCrc) {   // (two pairs per block: wave-local ordering only)
+			__builtin_amdgcn_s_waitcnt(0xc07f);   // the wave's reads of the old window are complete
+			__builtin_amdgcn_wave_barrier();
+		} else {
+			__syncthreads();   // the wave's reads of the old window are complete
+		}
 		// lane l's 16 bytes land at lds + 16*l (lane-linear).  Blocks past the
 		// stream end are skipped: their window bytes are never consumed, every
 		// use being bounded by |V| or |R|; a block holding any stream byte is
@@ -296,7 +314,11 @@ struct WinSrc {
 		const uint64_t tr0 = __builtin_amdgcn_s_memtime();
 #endif
 		vm_drain();        // the DMA landed (ordered by vmcnt) ...
-		__syncthreads();   // ... and is visible to every lane
+		if constexpr (kCrc) {
+			__builtin_amdgcn_wave_barrier();   // ... and is visible to every lane of the wave
+		} else {
+			__syncthreads();   // ... and is visible to every lane
+		}
 #ifdef DG_REFILL_PROF
 		refill_cycles += __builtin_amdgcn_s_memtime() - tr0;
 		++refill_count;
@@ -333,6 +355,97 @@ struct WinSrc {
 		}
 		PROF_ADD(*this, P_REFILLS, 1);
 		PROF_ADD(*this, P_T_REFILL, PROF_NOW_R() - t0);
+	}
+
+	// ── kCrc: the streams' CRC-64/XZ (delta.h:294-322) by the row fold of
+	//    dg_crc.h, with the five-bit tables at crc_tb ──
+	__device__ void crc_init(uint32_t tb) {
+		crc_tb = tb;
+#pragma unroll
+		for (uint32_t s = 0; s < 2; ++s) {
+			const uint32_t a1 = (len[s] + 15u) & ~15u;   // (|stream| < 4 GiB - 16)
+			crow_n[s] = (a1 + 511u) / 512u;
+			cdom[s] = (int32_t)(a1 - 512u * crow_n[s]);   // in (-512, 0]
+		}
+	}
+	// fold one row's pieces (lane l: the 8 bytes at stream offset o, zeros
+	// outside the stream, init = ~0 XOR-ed into the first 8 bytes)
+	__device__ __forceinline__ void crc_fold_piece(uint32_t s, int32_t o, uint64_t x) {
+		const uint32_t L = len[s];
+		if (o < 0 || (uint32_t)o >= L) x = 0ull;
+		else if ((uint32_t)o + 8u > L) x &= byte_mask(0, (int)(L - (uint32_t)o));   // past the end
+		if (o == 0) x = ~x;                                                          // init (|stream| >= 8)
+		crc_fold<kCrcFive, 8, 1>(cy_lo[s], cy_hi[s], 0u, 0u, (uint32_t)x, (uint32_t)(x >> 32), crc_tb, crc_tb);
+	}
+	// fold stream s's next rows while the window holds them (LDS reads);
+	// a row that started before the window (the window jumped past it) from
+	// memory; stops at the first row that reaches past the window, or past
+	// lim rows.  The window's bytes are the stream's (read-only) bytes, so
+	// any row inside it may be folded, ahead of the chain or behind it.
+	__device__ void crc_fold_window(uint32_t s, uint32_t lim) {
+		if (base[s] == 0xFFFF0000u) return;   // nothing loaded yet
+		const uint32_t lane = lane_id();
+		const uint32_t L = len[s];
+		const uint32_t wend = umin32(base[s] + kWin, L);   // window bytes that are stream bytes
+		const uint32_t stop = umin32(crow_n[s], lim);
+		while (crow[s] < stop) {
+			const int32_t rs = cdom[s] + (int32_t)(512u * crow[s]);
+			const int32_t o = rs + (int32_t)(8u * lane);
+			const uint32_t re = umin32((uint32_t)(rs + 512), L);   // (rs + 512 > 0)
+			if (re > wend) break;   // reaches past the window: a later call
+			uint64_t x = 0ull;
+			if (rs >= (int32_t)base[s] || (rs < 0 && base[s] == 0u)) {
+				if (o >= (int32_t)base[s] && (uint32_t)o < L) {
+					const lds_u32* w = (const lds_u32*)(win + (s ? kWinStride : 0) + ((uint32_t)o - base[s]));
+					x = ((uint64_t)w[1] << 32) | w[0];
+				}
+			} else if (o >= 0 && (uint32_t)o < L) {   // (the window moved past the row's start)
+				const uint2 g = *reinterpret_cast<const uint2*>(S[s] + o);
+				x = ((uint64_t)g.y << 32) | g.x;
+			}
+			crc_fold_piece(s, o, x);
+			++crow[s];
+		}
+	}
+	// between epochs (the chain's registers are few there): the rows the
+	// windows hold
+	__device__ __forceinline__ void crc_step() {
+		if constexpr (kCrc) {
+			crc_fold_window(0, 0xFFFFFFFFu);
+			crc_fold_window(1, 0xFFFFFFFFu);
+		}
+	}
+	// the rows no window held whole (the streams' ends, long jumps), from memory
+	__device__ void crc_fold_rest(uint32_t s) {
+		const uint32_t lane = lane_id();
+		const uint32_t L = len[s];
+		for (; crow[s] < crow_n[s]; ++crow[s]) {
+			const int32_t o = cdom[s] + (int32_t)(512u * crow[s] + 8u * lane);
+			uint64_t x = 0ull;
+			if (o >= 0 && (uint32_t)o < L) {
+				const uint2 g = *reinterpret_cast<const uint2*>(S[s] + o);
+				x = ((uint64_t)g.y << 32) | g.x;
+			}
+			crc_fold_piece(s, o, x);
+		}
+	}
+	// stream s's CRC-64/XZ (uniform): the remaining rows, the last row's
+	// advance, the per-lane x^(-64 l), the wave XOR, the end pad undone
+	__device__ uint64_t crc_final(uint32_t s, const uint64_t* tabs) {
+		const uint32_t L = len[s];
+		if (L < 8) {   // byte by byte (crc_finalize_kernel's short path)
+			uint64_t c = ~0ull;
+			for (uint32_t k = 0; k < L; ++k) c = tabs[(uint8_t)(c ^ S[s][k])] ^ (c >> 8);
+			return ~c;
+		}
+		crc_fold_window(s, 0xFFFFFFFFu);
+		crc_fold_rest(s);
+		crc_fold<kCrcFive, 8, 1>(cy_lo[s], cy_hi[s], 0u, 0u, 0u, 0u, crc_tb, crc_tb);
+		const uint64_t A = ((uint64_t)cy_hi[s] << 32) | cy_lo[s];
+		uint64_t acc = wave_xor64(A ? gf2_mulmod(A, tabs[kCrcRowK8 + lane_id()]) : 0ull);
+		const uint32_t t = ((L + 15u) & ~15u) - L;
+		if (t) acc = mul_nib(acc, tabs + 8 * 256 + kCrcLevels * kCrcNibTabWords + (1 + t) * kCrcNibTabWords);   // x^(-8t)
+		return ~acc;
 	}
 
 	// 4 bytes of stream s at offset x (little-endian), x inside the window
@@ -723,6 +836,7 @@ struct WinSrc {
 		return lim;
 	}
 };
+using WinSrc = WinSrcT<false>;
 
 // ───────────────────────────── the epoch chain ────────────────────────────
 
@@ -895,6 +1009,9 @@ __device__ __forceinline__ PairResult onepass_pair(Src& src, const EncodeArgs& a
 
 	while (scanning) {
 		skipA = false;
+#ifndef DG_NO_CRC_STEP
+		if constexpr (Src::kPhaseA) src.crc_step();   // (kCrc sources only)
+#endif
 		if (members && mem_live && v0 == r0 && v0 > s_cur) {
 			[[maybe_unused]] const uint64_t tr0 = PROF_NOW();
 			if constexpr (Src::kPhaseA) PROF_ADD(src, P_RESYNCS, 1);
@@ -1426,6 +1543,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 #endif
 }
 
+// onepass16_kernel for plain plans with both streams' CRC-64/XZ computed by
+// the pair's own wave (R and V read once, not again by a
+// CRC rows pass beside the kernel).  The wave folds, at every window refill,
+// the rows of 64 x 8 bytes its windows have moved past (from L2, where the
+// window loads left them) and the rest at the end; two pairs per block share
+// one copy of the five-bit row tables (3.25 KiB of LDS; a copy per wave does
+// not fit 16 waves per CU beside the windows).  The plan launches no CRC
+// pass for such a batch (dg_host.cpp, op_crc).
+constexpr uint32_t kOpCrcWaves = 2;
+__global__ __launch_bounds__(64 * kOpCrcWaves) __attribute__((amdgpu_waves_per_eu(4, 8))) void onepass16_crc_kernel(EncodeArgs a) {
+	__shared__ __attribute__((aligned(16))) uint8_t win[kOpCrcWaves][2 * kWinStride];
+	__shared__ uint32_t bm[kOpCrcWaves][256];
+	__shared__ __attribute__((aligned(4))) uint16_t lcache[kOpCrcWaves][kListCap];
+	__shared__ __attribute__((aligned(16))) uint8_t touch[kOpCrcWaves][kTouchAhead > 0 ? 256 : 4];
+	__shared__ __attribute__((aligned(256))) uint64_t T5[32 * kCrc5Tabs8];
+	for (uint32_t i = threadIdx.x; i < 32 * kCrc5Tabs8; i += 64 * kOpCrcWaves) T5[i] = a.crc_tab[kCrc5R8 + i];
+	__syncthreads();   // (the block's only barrier: each wave runs its own pair after it)
+	const uint32_t w = threadIdx.x >> 6;
+	const uint32_t pair = a.pair0 + blockIdx.x * kOpCrcWaves + w;
+	if (pair >= a.n_pairs) return;
+	const PairDev pd = a.pairs[pair];
+	const PairPlanDev pp = a.pplan[pair];
+	WinSrcT<true> src;
+	src.S[0] = a.ver + pd.v_off;
+	src.S[1] = a.ref + pd.r_off;
+	src.len[0] = (uint32_t)pd.v_len;
+	src.len[1] = (uint32_t)pd.r_len;
+	src.base[0] = src.base[1] = 0xFFFF0000u;   // nothing loaded yet (forces a fill)
+	src.win = (lds_u8*)win[w];
+	src.touch = (lds_u8*)touch[w];
+	src.lc = lcache[w];
+	src.powc = a.powc;
+	src.crc_init(lds_addr(T5));
+	PROF_INIT(src)
+	(void)onepass_pair<false, WinSrcT<true>, false>(src, a, pair, pd, pp, 16u, bm[w], (uint32_t*)lcache[w]);
+	vm_drain();   // no LDS-DMA may outlive the wave's use of its windows
+	const uint64_t cv = src.crc_final(0, a.crc_tab);
+	const uint64_t cr = src.crc_final(1, a.crc_tab);
+	if (lane_id() == 0) {   // (d_crc: per pair the CRC of R, then of V)
+		a.crc_out[2ull * pair] = cr;
+		a.crc_out[2ull * pair + 1] = cv;
+	}
+}
+
 // any seed length or alignment, bytes from HBM/L2
 template <int PF>
 __global__ __launch_bounds__(64, 4) void onepass_kernel(EncodeArgs a) {
@@ -1463,6 +1624,10 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 			if (g == 0) return hipSuccess;
 			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), op_lds_pad(), st, a);
 			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), op_lds_pad(), st, a);
+		} else if (a.crc_out) {   // plain plan, CRCs in the kernel
+			const uint32_t g = a.n_pairs - a.pair0;
+			if (g) hipLaunchKernelGGL(onepass16_crc_kernel, dim3((g + kOpCrcWaves - 1) / kOpCrcWaves),
+			                          dim3(64 * kOpCrcWaves), 0, st, a);
 		} else {
 			hipLaunchKernelGGL(onepass16_kernel<false>, dim3(a.n_pairs), dim3(64), op_lds_pad(), st, a);
 		}
