@@ -230,6 +230,7 @@ struct CrcArgs {
 	uint64_t* out;             // per span: CRC-64/XZ value
 	const uint64_t* xinv;      // 16 constants x^(-8t) mod P
 	uint64_t kseg;             // x^(8*kCrcSegBytes) mod P
+	const uint32_t* prio_flag; // member plans: set once the member kernel is done (rows pass to priority 1)
 };
 
 struct dg_decode_desc_dev {   // == dg_decode_desc_t

@@ -408,7 +408,7 @@ struct dg_encode_plan {
 	bool aligned16 = true;   // every pair offset a multiple of 16 (LDS-window kernel)
 	// device buffers
 	DevBuf d_pairs, d_pplan, d_powc, d_rec, d_nrec, d_dsize, d_crc_spans_r, d_crc_segs,
-	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls, d_gpairs;
+	    d_seg_crc, d_crc, d_tables, d_locks, d_tags, d_ctab, d_lookback, d_kcls, d_gpairs, d_prio_flag;
 	uint32_t n_gpairs = 0;       // correcting: pairs whose R index is built in memory
 	// onepass member mode (dg_members.hip): member arrays share the record
 	// slots' indexing; the verification work queue
@@ -582,6 +582,10 @@ static bool members_wanted(const dg_context_t* ctx, const dg_pair_t* pairs, uint
 	if (fm && fm[0] == '1') want = true;
 	return want;
 }
+#ifndef DG_CRC_PRIO_FLAG   // A/B: member plans raise the rows pass to priority 1 after the member kernel
+#define DG_CRC_PRIO_FLAG 0
+#endif
+constexpr bool kCrcPrioFlag = DG_CRC_PRIO_FLAG != 0;
 #ifndef DG_OP_CRC_DEFAULT   // 1 (A/B): onepass plain plans compute their CRCs in the onepass waves
 #define DG_OP_CRC_DEFAULT 0   // (measured slower: C2 1786 -> 1172 GiB/s, profiles/r06_experiments.md)
 #endif
@@ -870,6 +874,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		mbad |= P->d_cmap.alloc(8ull * std::max<uint32_t>(P->n_chunks, 1));
 		mbad |= P->d_seg.alloc(16ull * ((uint64_t)P->n_chunks + 2ull * n));
 		mbad |= P->d_nseg.alloc(4ull * std::max<uint32_t>(n, 1));
+		mbad |= P->d_prio_flag.alloc(4);
 		if (!mbad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
 			mbad = 1;
@@ -878,7 +883,7 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			// fits with the plain chain still gets a plan
 			(void)hipGetLastError();
 			for (DevBuf* b : {&P->d_mem_s, &P->d_srec, &P->d_nmem, &P->d_chunks, &P->d_csum, &P->d_cmap,
-			                  &P->d_seg, &P->d_nseg})
+			                  &P->d_seg, &P->d_nseg, &P->d_prio_flag})
 				b->release();
 			P->members = false;
 			P->n_chunks = 0;
@@ -1121,6 +1126,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
+		a.prio_flag = kCrcPrioFlag && P->members ? P->d_prio_flag.as<uint32_t>() : nullptr;
 		return a;
 	};
 #ifndef DG_CRC5_ALL   // A/B: the five-bit row pass beside the onepass kernel too
@@ -1203,6 +1209,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.n_mem = m.n_mem;
 				a.srec = m.srec;
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
+				if (kCrcPrioFlag) HIPCHK(ctx, hipMemsetD32Async(P->d_prio_flag.p, 1, 1, st));   // the rows pass to priority 1
 				HIPCHK(ctx, rec(6, st));
 				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
 			} else {
@@ -1247,6 +1254,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		if ((rc = run_crc()) != DG_OK) return rc;
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
 	} else {
+		if (kCrcPrioFlag && P->members) HIPCHK(ctx, hipMemsetD32Async(P->d_prio_flag.p, 0, 1, st));
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
 		if (P->crc_first) {   // A/B: CRC waves dispatched first

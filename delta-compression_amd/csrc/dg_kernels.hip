@@ -118,8 +118,18 @@ __global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
 	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
 	const uint32_t tb = lds_addr(T8);
 	const uint64_t kl = a.tables[kCrcRowK8 + lane];
+	bool raised = false;
 	for (uint32_t seg = uni(blockIdx.x * kCrcWavesPerBlock + wave); seg < a.n_segs;
 	     seg += gridDim.x * kCrcWavesPerBlock) {
+		if (a.prio_flag && !raised) {
+			// member plans: once the member kernel is done, the rows pass
+			// outranks the chains beside it (the routed plain chain's waves
+			// otherwise leave it the last issue slots)
+			if (uni(__hip_atomic_load(a.prio_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+				__builtin_amdgcn_s_setprio(1);
+				raised = true;
+			}
+		}
 		const CrcSegDev sd = a.segs[seg];
 		const CrcSpanDev sp = a.spans[sd.span];
 		const uint64_t c = crc_seg_rows<8, 1, DG_CRC_PF, kCrcSegBytes, false, TAB>(

@@ -45,8 +45,9 @@ FETCH_CLASS = {"onepass16_kernel": "dma16", "member_chunk_kernel": "dma16", "dec
 # pattern that matches names the pmc_calib class whose factor applies
 PATH_CLASS = [(r"onepass16_kernel|member_chunk_kernel|onepass_kernel", "dma16"),
               (r"crc_rows_wide", "stream16"), (r"crc_rows_kernel", "stream8"),
-              (r"correcting_build", "stream16"), (r"decode_kernel", "stream16"),
-              (r"serialize_wave_kernel|member_serialize_kernel", "dma4")]
+              (r"correcting_build", "stream16"), (r"decode_kernel", "stream16")]
+# (the serialisers mix 4-byte record loads, short unaligned payload reads and
+# staged V rows: no one class; they take the x1 lower and x2 upper readings)
 CALIB_DEFAULT = {"dma16": 2.0, "stream16": 2.0}
 
 
