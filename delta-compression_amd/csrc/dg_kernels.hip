@@ -82,14 +82,15 @@ __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __rest
 // pass that has the GPU to itself.  (Four bank-spread table copies, 128 KiB,
 // measured slower: 4.8 vs 5.1 TB/s alone, profiles/r05_crc_lab_product.txt.)
 constexpr uint32_t kCrcWideBlock = 1024;
-__global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a) {
+template <uint32_t kBlock = kCrcWideBlock>
+__global__ __launch_bounds__(kBlock) void crc_rows_wide_kernel(CrcArgs a) {
 	__shared__ __attribute__((aligned(256))) uint64_t TW[16 * 256];
-	for (uint32_t i = threadIdx.x; i < 16 * 256; i += kCrcWideBlock) TW[i] = a.tables[kCrcRows16 + i];
+	for (uint32_t i = threadIdx.x; i < 16 * 256; i += kBlock) TW[i] = a.tables[kCrcRows16 + i];
 	__syncthreads();
 	const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
 	const uint32_t tb = lds_addr(TW), tbh = tb + 8u * 2048u;
 	const uint64_t kl = a.tables[kCrcRowK16 + lane];
-	constexpr uint32_t kWaves = kCrcWideBlock / 64;
+	constexpr uint32_t kWaves = kBlock / 64;
 	for (uint32_t seg = uni(blockIdx.x * kWaves + wave); seg < a.n_segs; seg += gridDim.x * kWaves) {
 		const CrcSegDev sd = a.segs[seg];
 		const CrcSpanDev sp = a.spans[sd.span];
@@ -104,6 +105,9 @@ __global__ __launch_bounds__(kCrcWideBlock) void crc_rows_wide_kernel(CrcArgs a)
 // batches in flight), at most 64 VGPRs.
 #ifndef DG_CRC_PF
 #define DG_CRC_PF 2
+#endif
+#ifndef DG_CRC_BESIDE_WIDE
+#define DG_CRC_BESIDE_WIDE 0
 #endif
 #ifndef DG_CRC_PRIO   // A/B: issue priority of the rows pass beside another kernel (0..3)
 #define DG_CRC_PRIO 0
@@ -396,7 +400,7 @@ hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st) {
 hipError_t launch_crc_wide(const CrcArgs& a, uint32_t n_cu, hipStream_t st) {
 	if (a.n_segs) {
 		const uint32_t blocks = std::min<uint32_t>(n_cu, (a.n_segs + 15) / 16);
-		hipLaunchKernelGGL(crc_rows_wide_kernel, dim3(blocks), dim3(kCrcWideBlock), 0, st, a);
+		hipLaunchKernelGGL(crc_rows_wide_kernel<kCrcWideBlock>, dim3(blocks), dim3(kCrcWideBlock), 0, st, a);
 	}
 	if (a.n_spans)
 		hipLaunchKernelGGL(crc_finalize_kernel, dim3((a.n_spans + 63) / 64), dim3(64), 0, st, a);
@@ -419,6 +423,10 @@ hipError_t launch_crc(const CrcArgs& a, hipStream_t st, uint32_t overlap_cap, in
 		if (cap && blocks > cap) blocks = cap;
 		if (pass == kCrcPassRows5)
 			hipLaunchKernelGGL(crc_rows_kernel<kCrcFive>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
+#if DG_CRC_BESIDE_WIDE   // A/B: 16-byte pieces (32 KiB of tables) in one 4-wave block per CU beside the differencing
+		else if (cap)
+			hipLaunchKernelGGL(crc_rows_wide_kernel<256>, dim3(std::min<uint32_t>(blocks, cap / 2)), dim3(256), 0, st, a);
+#endif
 		else
 			hipLaunchKernelGGL(crc_rows_kernel<kCrcByte>, dim3(blocks), dim3(64 * kCrcWavesPerBlock), 0, st, a);
 	}

@@ -26,7 +26,7 @@ import tempfile
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "delta-compression_amd", "lib", "libdeltagpu.so")
+LIB = os.environ.get("DG_ISA_LIB") or os.path.join(ROOT, "delta-compression_amd", "lib", "libdeltagpu.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 KERNELS = ("serialize_wave_kernel", "member_serialize_kernel")
