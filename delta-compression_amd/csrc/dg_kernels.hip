@@ -101,10 +101,16 @@ __global__ __launch_bounds__(kBlock) void crc_rows_wide_kernel(CrcArgs a) {
 }
 
 // Beside another kernel: 8-byte pieces, one table copy (byte tables: 16 KiB;
-// five-bit tables: 3.25 KiB), DG_CRC_PF pieces per lane per batch (two
-// batches in flight), at most 64 VGPRs.
+// five-bit tables: 3.25 KiB), DG_CRC_PF (byte tables) / DG_CRC_PF5 (five-bit)
+// pieces per lane per batch (two batches in flight), at most 64 VGPRs.  Four
+// byte-table pieces per batch (58 VGPRs): C2 1762 -> 1801-1819 GiB/s beside
+// the onepass kernel (profiles/r06_experiments.md); the five-bit fold spills
+// at four, so it keeps two.
 #ifndef DG_CRC_PF
-#define DG_CRC_PF 2
+#define DG_CRC_PF 4
+#endif
+#ifndef DG_CRC_PF5
+#define DG_CRC_PF5 2
 #endif
 #ifndef DG_CRC_BESIDE_WIDE
 #define DG_CRC_BESIDE_WIDE 0
@@ -112,8 +118,11 @@ __global__ __launch_bounds__(kBlock) void crc_rows_wide_kernel(CrcArgs a) {
 #ifndef DG_CRC_PRIO   // A/B: issue priority of the rows pass beside another kernel (0..3)
 #define DG_CRC_PRIO 0
 #endif
+#ifndef DG_CRC_MINBLOCKS   // A/B: blocks per CU the register budget is sized for (8: 64 VGPRs)
+#define DG_CRC_MINBLOCKS 8
+#endif
 template <int TAB>
-__global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
+__global__ __launch_bounds__(256, DG_CRC_MINBLOCKS) void crc_rows_kernel(CrcArgs a) {
 	if constexpr (DG_CRC_PRIO > 0) __builtin_amdgcn_s_setprio(DG_CRC_PRIO);
 	constexpr uint32_t nt = TAB == kCrcByte ? 8 * 256 : 32 * kCrc5Tabs8;
 	__shared__ __attribute__((aligned(256))) uint64_t T8[nt];
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(256, 8) void crc_rows_kernel(CrcArgs a) {
 		}
 		const CrcSegDev sd = a.segs[seg];
 		const CrcSpanDev sp = a.spans[sd.span];
-		const uint64_t c = crc_seg_rows<8, 1, DG_CRC_PF, kCrcSegBytes, false, TAB>(
+		const uint64_t c = crc_seg_rows<8, 1, TAB == kCrcByte ? DG_CRC_PF : DG_CRC_PF5, kCrcSegBytes, false, TAB>(
 		    (uintptr_t)(a.arena[sp.which] + sp.off), sp.len, sp.nseg, sd.j, tb, tb, kl);
 		if (lane == 0) a.seg_crc[seg] = c;
 	}
