@@ -172,6 +172,7 @@ def pmc_path(config):
     upper readings, or None when the newest summary is of another library build."""
     import glob
     cur = lib_sha16()
+    stale = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_path_{config}.json")), reverse=True):
         try:
             d = json.load(open(f))
@@ -180,8 +181,8 @@ def pmc_path(config):
         if d.get("path_traffic_per_step"):
             if d.get("lib_sha16") and d["lib_sha16"] == cur:
                 return d, os.path.relpath(f, ROOT)
-            return None, f"stale: {os.path.relpath(f, ROOT)} was measured on another build of the library"
-    return None, None
+            stale = stale or os.path.relpath(f, ROOT)
+    return None, (f"stale: {stale} was measured on another build of the library" if stale else None)
 
 
 # ───────────────────────────── CPU baseline ─────────────────────────────────
