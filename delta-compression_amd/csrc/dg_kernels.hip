@@ -102,15 +102,16 @@ __global__ __launch_bounds__(kBlock) void crc_rows_wide_kernel(CrcArgs a) {
 
 // Beside another kernel: 8-byte pieces, one table copy (byte tables: 16 KiB;
 // five-bit tables: 3.25 KiB), DG_CRC_PF (byte tables) / DG_CRC_PF5 (five-bit)
-// pieces per lane per batch (two batches in flight), at most 64 VGPRs.  Four
-// byte-table pieces per batch (58 VGPRs): C2 1762 -> 1801-1819 GiB/s beside
-// the onepass kernel (profiles/r06_experiments.md); the five-bit fold spills
-// at four, so it keeps two.
+// pieces per lane per batch (two batches in flight), at most 72 VGPRs (a
+// register budget for 7 blocks per CU).  Four pieces per batch: byte tables
+// (58 VGPRs) C2 1762 -> 1801-1819 GiB/s beside the onepass kernel; five-bit
+// tables (67 VGPRs; at a 64-VGPR budget they spilled) c6 1340 -> 1358
+// (profiles/r06_experiments.md).
 #ifndef DG_CRC_PF
 #define DG_CRC_PF 4
 #endif
 #ifndef DG_CRC_PF5
-#define DG_CRC_PF5 2
+#define DG_CRC_PF5 4
 #endif
 #ifndef DG_CRC_BESIDE_WIDE
 #define DG_CRC_BESIDE_WIDE 0
@@ -118,8 +119,8 @@ __global__ __launch_bounds__(kBlock) void crc_rows_wide_kernel(CrcArgs a) {
 #ifndef DG_CRC_PRIO   // A/B: issue priority of the rows pass beside another kernel (0..3)
 #define DG_CRC_PRIO 0
 #endif
-#ifndef DG_CRC_MINBLOCKS   // A/B: blocks per CU the register budget is sized for (8: 64 VGPRs)
-#define DG_CRC_MINBLOCKS 8
+#ifndef DG_CRC_MINBLOCKS   // blocks per CU the register budget is sized for (7: 72 VGPRs, 8: 64)
+#define DG_CRC_MINBLOCKS 7
 #endif
 template <int TAB>
 __global__ __launch_bounds__(256, DG_CRC_MINBLOCKS) void crc_rows_kernel(CrcArgs a) {
