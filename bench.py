@@ -437,7 +437,9 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
         plan.set_timing(0)
     for _ in range(args.warmup):
         step()
+    modes0 = plan.run_modes
     elapsed = timed(R, args, step)
+    modes1 = plan.run_modes
     stages = plan.stage_times() if timing != "none" else {}
     plan.set_timing(0)
     elapsed = shard.max_over_ranks(R.dist, elapsed, R.world, "cuda")
@@ -446,11 +448,17 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     in_bytes_job = shard.sum_over_ranks(R.dist, in_bytes_rank, R.world, "cuda")
     value = in_bytes_job * args.steps / elapsed / 2**30
     members = plan.members
+    # automatic member mode over a batch it routes entirely to the plain chain:
+    # the timed runs go as a plain plan between member-mode probes
+    member_runs, plain_runs = modes1[0] - modes0[0], modes1[1] - modes0[1]
+    plain_runs_dominate = members and plain_runs > member_runs
     # the dominant kernel: the member kernel alone in member mode (its own
     # event pair), else the differencing kernel(s) of the "diff" stage
     diff_ms = stages.get("members", 0.0) if members else stages.get("diff", 0.0)
     chains_dominate = False
-    if members and stages.get("diff", 0.0) - stages.get("members", 0.0) > stages.get("members", 0.0):
+    if plain_runs_dominate:
+        diff_ms = stages.get("diff", 0.0) - stages.get("members", 0.0)
+    elif members and stages.get("diff", 0.0) - stages.get("members", 0.0) > stages.get("members", 0.0):
         # most pairs were routed to the plain chain (matches off diagonal 0):
         # the chain kernels after the member kernel dominate
         diff_ms = stages["diff"] - stages["members"]
@@ -461,7 +469,7 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
     delta_bytes = int(offs[-1].item())
     kname = ("correcting_build_kernel + correcting_scan_kernel" if algo == "correcting"
              else "onepass16_kernel (member chain + routed plain chain)" if chains_dominate
-             else "member_chunk_kernel" if members
+             else "member_chunk_kernel" if members and not plain_runs_dominate
              else "onepass16_kernel" if aligned16 else "onepass_kernel")
     traffic, traffic_src = pmc_traffic(name, kname) if npg == CONFIGS[name][0] else (None, None)
     # the path-level roofline of SURVEY §8(d) / BASELINE.md §3: every input
@@ -500,7 +508,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "table_size_floor": q,
             "q": plan.table_size(0),
             "seed_len": 16,
-            "onepass_chain": ("verified diagonal members" if members else "per-pair chain")
+            "onepass_chain": ((f"automatic: {plain_runs} of the {member_runs + plain_runs} timed runs as a plain "
+                               f"plan (the last member-mode run routed every pair to the per-pair chain), "
+                               f"{member_runs} member-mode probes" if plain_runs_dominate else
+                               "verified diagonal members") if members else "per-pair chain")
                              if algo == "onepass" else None,
             "delta_bytes_per_gpu": delta_bytes,
             "parallelism": f"dp{R.world} (pair shards, RCCL index scatter + size all-gather)",
@@ -521,6 +532,10 @@ def bench_encode(name, args, R, dg, ctx, shard, stream):
             "timing": ("HIP events on the run stream after the member kernel and after the chain "
                        "kernels (member chain, routed plain chain), mean over the timed steps"
                        if chains_dominate else
+                       "HIP events on the run stream around the chain kernels (plain runs: the plain "
+                       "chain; member-mode probes: the member and routed chains after the member "
+                       "kernel), mean over the timed steps"
+                       if plain_runs_dominate else
                        "HIP events on the run stream around the member kernel, mean over the timed "
                        "steps (the only events recorded in them)"
                        if members else

@@ -134,6 +134,7 @@ def _load() -> C.CDLL:
         "dg_encode_plan_output_bound": (u64, [vp]),
         "dg_encode_plan_num_pairs": (u32, [vp]),
         "dg_encode_plan_flags": (u32, [vp]),
+        "dg_encode_plan_run_modes": (C.c_int, [vp, C.POINTER(u64), C.POINTER(u64)]),
         "dg_encode_plan_table_size": (u64, [vp, u32]),
         "dg_encode_plan_run": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp]),
         "dg_encode_plan_set_timing": (C.c_int, [vp, C.c_int]),
@@ -294,6 +295,18 @@ class EncodePlan:
         """True when onepass runs through verified diagonal members."""
         fn = getattr(lib, "dg_encode_plan_flags", None)   # (absent from older A/B baselines)
         return bool(fn(self.handle) & 1) if fn else False
+
+    @property
+    def run_modes(self) -> tuple:
+        """(runs in member mode, runs as a plain plan) so far: automatic member
+        mode runs a batch whose every pair it routed to the plain chain as a
+        plain plan between member-mode probes (dg_encode_plan_run_modes)."""
+        fn = getattr(lib, "dg_encode_plan_run_modes", None)   # (absent from older A/B baselines)
+        if not fn:
+            return (0, 0)
+        m, p = C.c_uint64(), C.c_uint64()
+        self.ctx.check(fn(self.handle, C.byref(m), C.byref(p)), "dg_encode_plan_run_modes")
+        return (m.value, p.value)
 
     def table_size(self, i: int) -> int:
         return lib.dg_encode_plan_table_size(self.handle, i)

@@ -138,6 +138,9 @@ struct EncodeArgs {
 	// automatic member mode: pairs averaging fewer verified members per chunk
 	// than this run the plain chain (its records as one segment); 0 = never
 	uint32_t route_min;
+	// ... and the pairs so routed, counted by the routed chain (scan_sizes_kernel
+	// hands the count to the host and zeroes it; nullptr = not counted)
+	uint32_t* route_cnt;
 	// --verbose diagnostics (correcting; nullptr = off): per pair 8 u64 —
 	// build seeds passing the checkpoint, slots stored, scan checkpoints, fp
 	// mismatches, byte mismatches, matches, k, passing seeds whose slot is in
@@ -275,7 +278,10 @@ void print_verbose(const dg_encode_plan_t* P, uint32_t i, const uint64_t* stats,
                    size_t delta_len);
 
 // launchers (dg_kernels.hip)
-hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st);
+// (member plans: routed_after, when set, is waited for between the member
+// chain's launch and the routed plain chain's)
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st,
+                          hipEvent_t routed_after = nullptr);
 bool onepass16_selected();   // false when DG_ONEPASS_GLOBAL=1 forces the HBM-direct kernel
 hipError_t launch_members(const SpecArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
 hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint32_t n_cu, hipStream_t st);
@@ -284,7 +290,9 @@ hipError_t launch_member_serialize(const MemSerArgs& a, uint32_t n_chunks, uint3
 hipError_t launch_correcting_clear(const EncodeArgs& a, hipStream_t st);
 hipError_t launch_correcting(const EncodeArgs& a, uint32_t p, hipStream_t st, uint32_t lds_cap, uint64_t qmin,
                              hipEvent_t ev_built, hipEvent_t ev_fork);
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st);
+// (route_cnt / route_fb: the routed-pair count moved to a host-mapped word)
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st,
+                       uint32_t* route_cnt = nullptr, uint32_t* route_fb = nullptr);
 hipError_t launch_serialize_wave(const SerArgs& s, hipStream_t st);   // wave per pair, CRCs patched after
 hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_t* crc,
                             const int32_t* status, uint32_t n, hipStream_t st);

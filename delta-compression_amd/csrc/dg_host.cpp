@@ -388,6 +388,32 @@ struct DevBuf {
 	template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// one u32 of mapped, coherent host memory the device writes (h: host address,
+// d: its device address)
+struct HostWord {
+	uint32_t* h = nullptr;
+	uint32_t* d = nullptr;
+	~HostWord() { release(); }
+	void release() {
+		if (h) hipHostFree(h);
+		h = d = nullptr;
+	}
+	int alloc() {
+		release();
+		if (hipHostMalloc((void**)&h, 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+			h = nullptr;
+			return -1;
+		}
+		*h = 0;
+		if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) {
+			release();
+			return -1;
+		}
+		return 0;
+	}
+	uint32_t read() const { return __atomic_load_n(h, __ATOMIC_RELAXED); }
+};
+
 }  // namespace
 
 // ───────────────────────────── encode plan ────────────────────────────────
@@ -421,6 +447,7 @@ struct dg_encode_plan {
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	bool serial_crc = false;   // DG_SERIAL_CRC=1: CRC on the run stream (A/B)
 	bool crc_first = false;    // DG_CRC_FIRST=1: enqueue the CRC before the differencing (A/B)
+	bool chain_join = false;   // DG_CHAIN_JOIN=1: member plans' routed chain always waits for the CRC pass (A/B)
 	bool crc_late_fin = true;  // member plans: the CRC's combine after the chains (DG_CRC_JOIN=0: not, A/B)
 	bool crc_patch = false;    // DG_CRC_PATCH=1: header CRCs by crc_patch_kernel after the serialiser (A/B)
 	bool skip_crc = false;     // DG_SKIP_CRC=1: no CRC kernels, wrong header CRCs (A/B bound only)
@@ -430,6 +457,13 @@ struct dg_encode_plan {
 	bool crc_wide = false;     // correcting: R's and V's CRC in one wide-table pass before the build
 	bool crc_wide_beside = false;   // ... or forked after the build, beside the V scan
 	uint32_t route_min = 0;    // member mode chosen automatically: route poorly verified pairs to the plain chain
+	// automatic member mode: the routed-pair count of the last completed run
+	// (written by scan_sizes_kernel into mapped host memory) decides whether the
+	// routed chain waits for the CRC pass (see the run)
+	DevBuf d_route_cnt;
+	HostWord route_fb;
+	uint32_t plain_streak = 0;   // runs since the last member-mode probe (dg_encode_plan_run)
+	uint64_t member_runs = 0, plain_runs = 0;   // dg_encode_plan_run_modes
 	uint64_t* stats = nullptr; // dg_encode_plan_set_stats: --verbose counters (device, 8 per pair)
 	uint64_t qmin = ~0ull;
 	uint64_t v_total = 0;      // sum |V| of the batch
@@ -875,6 +909,11 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 		mbad |= P->d_seg.alloc(16ull * ((uint64_t)P->n_chunks + 2ull * n));
 		mbad |= P->d_nseg.alloc(4ull * std::max<uint32_t>(n, 1));
 		mbad |= P->d_prio_flag.alloc(4);
+		if (P->route_min) {
+			mbad |= P->d_route_cnt.alloc(4);
+			mbad |= P->route_fb.alloc();
+			if (!mbad && hipMemset(P->d_route_cnt.p, 0, 4) != hipSuccess) mbad = 1;
+		}
 		if (!mbad && !jobs.empty() &&
 		    hipMemcpy(P->d_chunks.p, jobs.data(), 4 * jobs.size(), hipMemcpyHostToDevice) != hipSuccess)
 			mbad = 1;
@@ -883,8 +922,9 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 			// fits with the plain chain still gets a plan
 			(void)hipGetLastError();
 			for (DevBuf* b : {&P->d_mem_s, &P->d_srec, &P->d_nmem, &P->d_chunks, &P->d_csum, &P->d_cmap,
-			                  &P->d_seg, &P->d_nseg, &P->d_prio_flag})
+			                  &P->d_seg, &P->d_nseg, &P->d_prio_flag, &P->d_route_cnt})
 				b->release();
+			P->route_fb.release();
 			P->members = false;
 			P->n_chunks = 0;
 			mbad = 0;
@@ -918,6 +958,8 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 	P->dbg = db ? (uint32_t)strtoul(db, nullptr, 0) : 0;
 	const char* cf = ab_env("DG_CRC_FIRST");
 	P->crc_first = cf && cf[0] == '1';
+	const char* chj = ab_env("DG_CHAIN_JOIN");
+	P->chain_join = chj && chj[0] == '1';
 	const char* cj = ab_env("DG_CRC_JOIN");
 	if (cj) P->crc_late_fin = cj[0] != '0';
 	const char* cp = ab_env("DG_CRC_PATCH");
@@ -943,6 +985,12 @@ int dg_encode_plan_create(dg_context_t* ctx, dg_algorithm_t algo, const dg_pair_
 uint64_t dg_encode_plan_output_bound(const dg_encode_plan_t* P) { return P ? P->out_bound : 0; }
 uint32_t dg_encode_plan_num_pairs(const dg_encode_plan_t* P) { return P ? P->n : 0; }
 uint32_t dg_encode_plan_flags(const dg_encode_plan_t* P) { return P && P->members ? DG_PLAN_MEMBERS : 0u; }
+int dg_encode_plan_run_modes(const dg_encode_plan_t* P, uint64_t* member_runs, uint64_t* plain_runs) {
+	if (!P || !member_runs || !plain_runs) return DG_ERR_INVALID_ARG;
+	*member_runs = P->member_runs;
+	*plain_runs = P->plain_runs;
+	return DG_OK;
+}
 
 int dg_encode_plan_set_stats(dg_encode_plan_t* P, uint64_t* d_stats) {
 	if (!P) return DG_ERR_INVALID_ARG;
@@ -1080,6 +1128,10 @@ static MemSerArgs mem_ser_args(const dg_encode_plan_t* P, const uint8_t* d_ver, 
 	return m;
 }
 
+// automatic member mode over a batch the member kernel gains nothing on: one
+// run in this many runs in member mode (the others as a plain plan)
+constexpr uint32_t kProbeEvery = 16;
+
 int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t* d_ver,
                        uint8_t* d_out, uint64_t out_cap, uint64_t* d_offsets, int32_t* d_status,
                        void* stream) {
@@ -1112,7 +1164,29 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// stream for the chains.  Enqueued right after the row pass, its waves
 	// queue behind the chains' full grid and slowed the routed chain of c3s
 	// by 13 % (40.9 vs 36.2 ms, profiles/r05_experiments.md).
-	const bool late_fin = P->members && P->crc_late_fin && !serial && !P->crc_wide && !P->fused;
+	// Automatic member mode: a batch whose every pair the last completed
+	// member-mode run of this plan routed to the plain chain (shift and
+	// transposition pairs, c3s / c4o) runs as a plain plan, the member kernel
+	// and its serialiser skipped, except every kProbeEvery-th run, which
+	// refreshes the count.  (A hint only: the output bytes do not depend on
+	// it.)
+	bool mem = P->members;
+	if (mem && P->route_min && P->route_fb.read() >= P->n) {
+		if (++P->plain_streak < kProbeEvery) mem = false;
+		else P->plain_streak = 0;
+	}
+	++(mem ? P->member_runs : P->plain_runs);
+	const bool late_fin = mem && P->crc_late_fin && !serial && !P->crc_wide && !P->fused;
+	// automatic member mode: when the last completed run of this plan routed
+	// more pairs to the plain chain than one round of chains fills (16 per
+	// CU), the routed chain's grid waits for the CRC pass to end.  Dispatched
+	// beside the pass's resident blocks, the chains land unevenly over the
+	// SIMDs and the second round's last pairs trail: c3s 39.1 -> 35.7 ms
+	// (profiles/r06_experiments.md).  Batches that route fewer pairs keep the
+	// pass beside the member chain, whose shadow it is at c6.  (A hint only:
+	// the run's bytes do not depend on it.)
+	const bool chain_join = mem && !serial && !P->skip_crc &&
+	                        (P->chain_join || (P->route_min && P->route_fb.read() > 16u * ctx->n_cu));
 	auto crc_args = [&]() {
 		CrcArgs a{};
 		a.arena[0] = d_ref;
@@ -1126,7 +1200,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		a.out = P->d_crc.as<uint64_t>();
 		a.xinv = ctx->d_xinv;
 		a.kseg = ctx->kseg;
-		a.prio_flag = kCrcPrioFlag && P->members ? P->d_prio_flag.as<uint32_t>() : nullptr;
+		a.prio_flag = kCrcPrioFlag && mem ? P->d_prio_flag.as<uint32_t>() : nullptr;
 		return a;
 	};
 #ifndef DG_CRC5_ALL   // A/B: the five-bit row pass beside the onepass kernel too
@@ -1151,7 +1225,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 			// with its whole grid; capped at 2 blocks per CU it took 0.97 ms
 			// there instead of 0.71: C4 731 -> 813 GiB/s)
 			else HIPCHK(ctx, launch_crc(a, cs, P->serial_crc || P->crc_fused ? 0u : 2u * ctx->n_cu * std::max(rounds, 1u),
-			                            P->members || kCrc5All ? kCrcPassRows5 : kCrcPassRows, !late_fin));
+			                            mem || kCrc5All ? kCrcPassRows5 : kCrcPassRows, !late_fin));
 		}
 		HIPCHK(ctx, rec(1, cs));
 		return DG_OK;
@@ -1159,7 +1233,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	// differencing -> COPY records + per-pair delta sizes
 	auto run_diff = [&]() -> int {
 		HIPCHK(ctx, rec(2, st));
-		if (!P->members) HIPCHK(ctx, rec(6, st));
+		if (!mem) HIPCHK(ctx, rec(6, st));
 		EncodeArgs a{};
 		a.ref = d_ref;
 		a.ver = d_ver;
@@ -1188,7 +1262,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				a.lookback = P->d_lookback.as<unsigned long long>();
 				HIPCHK(ctx, hipMemsetAsync(P->d_lookback.p, 0, 8ull * P->n, st));
 			}
-			if (P->members) {
+			if (mem) {
 				SpecArgs m{};
 				m.ref = d_ref;
 				m.ver = d_ver;
@@ -1211,7 +1285,8 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 				HIPCHK(ctx, launch_members(m, P->n_chunks, ctx->n_cu, st));
 				if (kCrcPrioFlag) HIPCHK(ctx, hipMemsetD32Async(P->d_prio_flag.p, 1, 1, st));   // the rows pass to priority 1
 				HIPCHK(ctx, rec(6, st));
-				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st));
+				if (P->route_min) a.route_cnt = P->d_route_cnt.as<uint32_t>();
+				HIPCHK(ctx, launch_onepass(a, a.p, P->aligned16, st, chain_join ? P->ev_join : nullptr));
 			} else {
 				if (P->op_crc) {
 					a.crc_out = P->d_crc.as<uint64_t>();
@@ -1254,11 +1329,12 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		if ((rc = run_crc()) != DG_OK) return rc;
 		HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
 	} else {
-		if (kCrcPrioFlag && P->members) HIPCHK(ctx, hipMemsetD32Async(P->d_prio_flag.p, 0, 1, st));
+		if (kCrcPrioFlag && mem) HIPCHK(ctx, hipMemsetD32Async(P->d_prio_flag.p, 0, 1, st));
 		HIPCHK(ctx, hipEventRecord(P->ev_fork, st));
 		HIPCHK(ctx, hipStreamWaitEvent(cs, P->ev_fork, 0));
-		if (P->crc_first) {   // A/B: CRC waves dispatched first
+		if (P->crc_first || chain_join) {   // CRC waves dispatched first (A/B), or the routed chain after them
 			if ((rc = run_crc()) != DG_OK) return rc;
+			if (chain_join) HIPCHK(ctx, hipEventRecord(P->ev_join, cs));
 			if ((rc = run_diff()) != DG_OK) return rc;
 		} else {
 			if ((rc = run_diff()) != DG_OK) return rc;
@@ -1276,7 +1352,8 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 		return DG_OK;
 	}
 	// 3. exclusive scan of sizes -> packed offsets
-	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st));
+	HIPCHK(ctx, launch_scan(P->d_dsize.as<uint64_t>(), d_offsets, P->n, st,
+	                        mem && P->route_min ? P->d_route_cnt.as<uint32_t>() : nullptr, P->route_fb.d));
 	SerArgs s{};
 	s.ver = d_ver;
 	s.pairs = P->d_pairs.as<PairDev>();
@@ -1294,7 +1371,7 @@ int dg_encode_plan_run(dg_encode_plan_t* P, const uint8_t* d_ref, const uint8_t*
 	//    (the CRC stream may still be running beside the chains), then join
 	//    and patch them in; the others join first (below)
 	HIPCHK(ctx, rec(4, st));
-	if (P->members) {   // the chains' segment lists, one wave per chunk
+	if (mem) {   // the chains' segment lists, one wave per chunk
 		const MemSerArgs m = mem_ser_args(P, d_ver, d_out, out_cap, d_offsets, d_status);
 		HIPCHK(ctx, launch_member_serialize(m, P->n_chunks, ctx->n_cu, st));
 		if (!serial) HIPCHK(ctx, hipStreamWaitEvent(st, P->ev_join, 0));   // join the CRCs

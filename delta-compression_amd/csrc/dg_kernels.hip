@@ -40,9 +40,16 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
 }
 
 __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint64_t* __restrict__ sz,
-                                                          uint64_t* __restrict__ off, uint32_t n) {
+                                                          uint64_t* __restrict__ off, uint32_t n,
+                                                          uint32_t* route_cnt, uint32_t* route_fb) {
 	__shared__ uint64_t wsum[16];
 	const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = lane_id();
+	if (route_cnt && tid == 0) {
+		// member plans: the pairs the run routed to the plain chain, for the
+		// host's next run (dg_host.cpp, chain_join); zeroed for that run
+		__hip_atomic_store(route_fb, *route_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+		*route_cnt = 0u;
+	}
 	const uint32_t per = (n + 1023) / 1024;
 	const uint32_t b = tid * per, e = min(b + per, n);
 	uint64_t s = 0;
@@ -392,8 +399,9 @@ hipError_t launch_crc_patch(uint8_t* out, const uint64_t* offsets, const uint64_
 	return hipGetLastError();
 }
 
-hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st) {
-	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n);
+hipError_t launch_scan(const uint64_t* sz, uint64_t* off, uint32_t n, hipStream_t st, uint32_t* route_cnt,
+                       uint32_t* route_fb) {
+	hipLaunchKernelGGL(scan_sizes_kernel, dim3(1), dim3(1024), 0, st, sz, off, n, route_cnt, route_fb);
 	return hipGetLastError();
 }
 

@@ -1477,6 +1477,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DG_WAVES_PER
 			for (uint32_t c = lane_id(); c < nch; c += 64) v += a.csum[2ull * (pp.chunk_base + c)];
 			const bool member_pair = rdlane(wave_incl_scan(v), 63) >= a.route_min * nch;
 			if (member_pair != kMembers) return;
+			if (kRouted && a.route_cnt && lane_id() == 0) atomicAdd(a.route_cnt, 1u);
 		}
 	}
 	WinSrc src;
@@ -1615,7 +1616,7 @@ static uint32_t op_lds_pad() {
 	return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
 }
 
-hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st) {
+hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipStream_t st, hipEvent_t routed_after) {
 	if (a.n_pairs == 0) return hipSuccess;
 	if (p == 16 && aligned16 && !force_global_src()) {
 		if (a.srec) {   // member plan: the member chain, and the plain chain for routed pairs
@@ -1623,7 +1624,13 @@ hipError_t launch_onepass(const EncodeArgs& a, uint32_t p, bool aligned16, hipSt
 			const uint32_t g = a.n_pairs - a.pair0;
 			if (g == 0) return hipSuccess;
 			hipLaunchKernelGGL(onepass16_kernel<true>, dim3(g), dim3(64), op_lds_pad(), st, a);
-			if (a.route_min) hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), op_lds_pad(), st, a);
+			if (a.route_min) {
+				if (routed_after) {
+					const hipError_t e = hipStreamWaitEvent(st, routed_after, 0);
+					if (e != hipSuccess) return e;
+				}
+				hipLaunchKernelGGL((onepass16_kernel<false, true>), dim3(g), dim3(64), op_lds_pad(), st, a);
+			}
 		} else if (a.crc_out) {   // plain plan, CRCs in the kernel
 			const uint32_t g = a.n_pairs - a.pair0;
 			if (g) hipLaunchKernelGGL(onepass16_crc_kernel, dim3((g + kOpCrcWaves - 1) / kOpCrcWaves),

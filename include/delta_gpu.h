@@ -226,6 +226,12 @@ int dg_encode_plan_set_stats(dg_encode_plan_t *plan, uint64_t *d_stats);
  * diagonal members (DG_LIMIT_ONEPASS_MEMBERS). */
 #define DG_PLAN_MEMBERS 1u
 uint32_t dg_encode_plan_flags(const dg_encode_plan_t *plan);
+/* The plan's runs so far by how they ran: in member mode, and as a plain plan
+ * (every run of a plan without member mode; in automatic member mode, the
+ * runs of a batch whose every pair the last completed member-mode run routed
+ * to the plain chain, between member-mode probes every 16th run).  The output
+ * bytes are the same either way.  Returns DG_OK or DG_ERR_INVALID_ARG. */
+int dg_encode_plan_run_modes(const dg_encode_plan_t *plan, uint64_t *member_runs, uint64_t *plain_runs);
 /* Per-pair command statistics of the last run (device pointers owned by the
  * plan, valid until the next run): number of COPY commands and delta size. */
 const uint32_t *dg_encode_plan_copy_counts_device(const dg_encode_plan_t *plan);
