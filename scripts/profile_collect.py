@@ -138,8 +138,13 @@ def main():
         bj = os.path.join(src, f"pmc_{cfg}_FETCH_SIZE.json")
         bline = json.load(open(bj)) if os.path.exists(bj) else {}
         kname = bline.get("roofline", {}).get("kernel")
-        raw_f = sum(f.values()) * 1024
-        raw_w = sum(w.values()) * 1024
+        # the line's dominant kernel(s) only: a pass may also hold other
+        # kernels the include regex admits (c3s / c4o plain runs: the member
+        # kernel and chains of the member-mode probes)
+        pats = DOMINANT.get(kname)
+        dom = (lambda k: any(re.search(p, k) for p in pats)) if pats else (lambda k: True)
+        raw_f = sum(v for k, v in f.items() if dom(k)) * 1024
+        raw_w = sum(v for k, v in w.items() if dom(k)) * 1024
         cls = FETCH_CLASS.get(kname, "dma16")
         fac = (calib.get(cls) or {}).get("bytes_per_fetch_kib") or 2.0
         # the table tier's random 16-byte loads: pmc_calib shows FETCH_SIZE
